@@ -1,0 +1,146 @@
+/*
+ * masurvival.h -- C-ABI of the MI355X-native batched MaSurvival env step.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   MaSurvival.step  (reference: masurvival/envs/masurvival_env.py:76-90)
+ *   -> Simulation.step (reference: masurvival/simulation.py:233-242)
+ * batched over N independent envs that live in HBM as struct-of-arrays.
+ *
+ * Plain C types only: every I/O pointer is a DEVICE pointer owned by the
+ * caller unless stated otherwise; `stream` is a hipStream_t passed as void*.
+ * Calls are stream-ordered and asynchronous (no implicit device sync) and are
+ * not re-entrant per handle.  Errors: 0 = ok, negative = error code, with a
+ * thread-local message from mas_last_error().  Nothing aborts or throws
+ * across this ABI.
+ */
+#ifndef MASURVIVAL_H
+#define MASURVIVAL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAS_ABI_VERSION 1
+
+#define MAS_OK 0
+#define MAS_ERR_INVALID_ARG (-1)
+#define MAS_ERR_UNSUPPORTED (-2)
+#define MAS_ERR_HIP (-3)
+#define MAS_ERR_OOM (-4)
+
+#define MAS_MAX_ZONE_PHASES 8
+
+/* Resolved env configuration: the POD lowering of onevsone_heals_config
+ * (reference masurvival_env.py:140-238) after MaSurvival.__init__'s rewrites
+ * (masurvival_env.py:293-389).  The Python front-end (masurvival.config)
+ * builds it with the reference's one-level merge semantics. */
+typedef struct mas_config {
+    int32_t n_agents;          /* agents.n_agents                 (:166-169) */
+    int32_t n_heals;           /* heals.reset_spawns.n_items      (:210-214) */
+    int32_t n_boxes;           /* boxes.reset_spawns.n_boxes      (:191-195) */
+    int32_t teams;             /* teams.twoteams -> TwoTeams       (:340-342) */
+    int32_t ownership;         /* boxes.ownership -> OwnedObject*  (:196,345) */
+    int32_t melee_cooldown;    /* >0: Melee(cooldown); 0: ContinuousMelee (:309-312) */
+    int32_t omniscient;        /* observation.omniscent            (:141-143) */
+    int32_t gameover_mode;     /* 0 = 'alldead', 1 = 'lastalive'   (:154-156) */
+    float r_alive, r_dead, r_kill, r_death; /* reward_scheme      (:144-153) */
+    int32_t grid_size;         /* spawn_grid.grid_size             (:158-161) */
+    double floor_size;         /* spawn_grid.floor_size (= room size) */
+    double agent_size;         /* agents.agent_size (diameter)     (:168) */
+    float impulse[3];          /* motors.impulse                   (:177-180) */
+    int32_t agent_health;      /* health.health                    (:181-183) */
+    float melee_range;         /* melee.range                      (:184-190) */
+    int32_t melee_damage;      /* melee.damage */
+    double box_size;           /* boxes.reset_spawns.box_size */
+    int32_t box_health;        /* boxes.health                     (:208) */
+    int32_t randomized_boxes;  /* 'randomized_shape' in boxes      (:362-366) */
+    double avg_w, std_w, avg_h, std_h, min_w, min_h; /* RandomizeBoxShapes (semantics.py:97-120) */
+    double box_item_size;      /* boxes.item.item_size             (:204-207) */
+    float box_item_offset;     /* boxes.item.offset */
+    double heal_size;          /* heals.reset_spawns.item_size */
+    int32_t healing;           /* heals.heal.healing               (:215-217) */
+    int32_t slots;             /* inventory.slots                  (:219-221) */
+    float pickup_radius;       /* auto_pickup.shape = circle(0.5)  (:222-224) */
+    float give_radius;         /* give.shape = circle(2)           (:225-227) */
+    float deathdrop_radius;    /* death_drop.radius                (:228-230) */
+    int32_t zone_phases;       /* safe_zone.phases                 (:231-237) */
+    int32_t zone_cooldown;
+    int32_t zone_damage;
+    int32_t zone_n_radii;      /* len(safe_zone.radiuses) (a 0 radius is appended) */
+    double zone_radii[MAS_MAX_ZONE_PHASES];
+    int32_t zone_random_centers; /* centers == 'random' */
+    float zone_centers[MAS_MAX_ZONE_PHASES][2]; /* used when !zone_random_centers */
+    float cam_depth;           /* cameras.depth                    (:173-176) */
+    double cam_fov;            /* cameras.fov (radians, double as in Python) */
+    double wall_aspect_ratio;  /* ThickRoomWalls default 100 (semantics.py:685) */
+} mas_config;
+
+/* Observation layout: one flat float32 row of `obs_dim` per agent; the keys
+ * are laid out in observation_space (gym Dict, sorted-key) order, each key's
+ * per-agent sub-array flattened C-order (compute_obs_space :391-447). */
+#define MAS_MAX_KEYS 16
+typedef struct mas_obs_layout {
+    int32_t n_agents;
+    int32_t obs_dim;
+    int32_t n_keys;
+    char key_name[MAS_MAX_KEYS][24];
+    int32_t key_offset[MAS_MAX_KEYS];   /* float offset inside the row */
+    int32_t key_ndim[MAS_MAX_KEYS];     /* ndim of the per-agent sub-array */
+    int32_t key_shape[MAS_MAX_KEYS][2]; /* per-agent sub-array shape */
+} mas_obs_layout;
+
+typedef struct mas_handle mas_handle;
+
+/* replaces MaSurvival.__init__ (masurvival_env.py:293-389): validates the
+ * config, allocates the SoA state of n_envs envs on `device` (HBM-resident,
+ * no allocation afterwards). */
+int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle** out);
+int mas_destroy(mas_handle* h);
+
+/* replaces compute_obs_space (masurvival_env.py:391-447). */
+int mas_get_obs_layout(const mas_handle* h, mas_obs_layout* out);
+int64_t mas_num_envs(const mas_handle* h);
+
+/* replaces the np_random assignment (masurvival_env.py:50,67,455-465):
+ * per-env numpy PCG64 bit-generator state, HOST array [n_envs][6] of
+ * {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger}
+ * (numpy.random.PCG64().state).  One stream per env, shared by the spawn
+ * shuffle, box shapes, zone centres and death drops as in the reference. */
+int mas_seed(mas_handle* h, const uint64_t* host_rng_states, void* stream);
+
+/* replaces BaseEnv.reset (masurvival_env.py:59-74) for every env whose
+ * env_mask byte is non-zero (env_mask == NULL: all envs).  Writes the reset
+ * observation rows of those envs into obs [n_envs][n_agents][obs_dim]. */
+int mas_reset(mas_handle* h, const uint8_t* env_mask, float* obs, void* stream);
+
+/* replaces BaseEnv.step (masurvival_env.py:76-90): actions int8
+ * [n_envs][n_agents][6] (MultiDiscrete [3,3,3,2,2,2], dead agents ignored),
+ * writes obs [n_envs][n_agents][obs_dim], rewards [n_envs][n_agents],
+ * done [n_envs].  auto_reset != 0: an env that is done is reset in the same
+ * launch and its obs rows hold the first observation of the new episode
+ * (rewards/done still describe the finished step). */
+int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards,
+             uint8_t* done, int32_t auto_reset, void* stream);
+
+/* Per-env episode statistics (flush_stats, masurvival_env.py:471-508):
+ * device float [n_envs][MAS_STATS_WIDTH] laid out as
+ * reward0..reward{R-1}, kills0..kills{R-1}, steps, heals_used, boxes_placed
+ * with R = 2 (teams) or n_agents.  Accumulated since the last flush. */
+#define MAS_STATS_WIDTH 19
+int mas_flush_stats(mas_handle* h, float* stats, void* stream);
+
+/* Raw SoA state image (checkpoint / parity state injection).  Byte size of
+ * the image and copies to/from a caller DEVICE buffer of that size. */
+int64_t mas_state_bytes(const mas_handle* h);
+int mas_get_state(mas_handle* h, void* dst, void* stream);
+int mas_set_state(mas_handle* h, const void* src, void* stream);
+
+const char* mas_last_error(void);
+int32_t mas_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MASURVIVAL_H */

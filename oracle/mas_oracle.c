@@ -1,0 +1,2307 @@
+/*
+ * mas_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * Scalar C restatement of the reference MaSurvival step for ONE env:
+ *   rules / obs / rewards : reference masurvival/semantics.py, simulation.py,
+ *                           envs/masurvival_env.py (cited per function)
+ *   physics               : Box2D 2.3.x (third-party, inside PyBox2D 2.3.10,
+ *                           NOT vendored in /root/reference, not installed
+ *                           here) restated from the published upstream
+ *                           algorithm for the subset MaSurvival uses
+ *                           (SURVEY.md Appendix B).  "Box2D:" comments name
+ *                           the upstream routine being restated.
+ *   RNG                   : numpy Generator(PCG64) (random, shuffle, normal)
+ *                           restated bit-exactly (validated against numpy in
+ *                           tests/test_oracle_rng.py).
+ *
+ * Determinism contract shared with the HIP path (both built with
+ * -ffp-contract=off, IEEE division/sqrt): identical float op order, a shared
+ * double-precision sin/cos (ora_sincos) in place of libm sinf/cosf, and one
+ * canonical order where Box2D's is an implementation detail of its dynamic
+ * tree / contact lists (documented in DESIGN.md "Canonical orders"):
+ *   queries & ray casts : groups in dict order boxes, box_items, heals,
+ *                         walls, agents; bodies in group list order
+ *   contact solver      : agent-agent pairs (i<j) then agent-static pairs
+ *                         (agent-major; statics = walls then boxes)
+ * Nothing in the product (gym-ma-survival-2d_amd/) links or loads this file.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mas_oracle.h"
+#include "ziggurat_tables.h"
+
+typedef ora_v2 v2;
+typedef ora_rot rot;
+typedef ora_poly poly;
+
+/* ------------------------------------------------------------------ */
+/* Box2D b2Math / b2Settings                                          */
+/* ------------------------------------------------------------------ */
+#define B2_PI 3.14159265359f
+#define LINEAR_SLOP 0.005f
+#define POLYGON_RADIUS (2.0f * LINEAR_SLOP)
+#define BAUMGARTE 0.2f
+#define TOI_BAUMGARTE 0.75f
+#define MAX_LINEAR_CORRECTION 0.2f
+#define MAX_TRANSLATION 2.0f
+#define MAX_ROTATION (0.5f * B2_PI)
+#define TIME_TO_SLEEP 0.5f
+#define LINEAR_SLEEP_TOL 0.01f
+#define ANGULAR_SLEEP_TOL (2.0f / 180.0f * B2_PI)
+#define MAX_SUB_STEPS 8
+#define VELOCITY_THRESHOLD 1.0f
+
+/* coverage counters (tests assert the golden fixtures exercise each path) */
+enum { CNT_TOI_EVENT, CNT_TOI_RESTORE, CNT_SLEEP, CNT_BOX_BROKEN, CNT_BOX_PLACED, CNT_ITEM_PICKED,
+       CNT_GIVE_OK, CNT_GIVE_LOST, CNT_DROP_ITEMS, CNT_HEAL_USED, CNT_DOUBLE_PICK, CNT_AA_CONTACT, CNT_N };
+static __thread int64_t g_cnt[CNT_N];
+void ora_counters(int64_t* out, int32_t reset)
+{
+    for (int k = 0; k < CNT_N; ++k) out[k] = g_cnt[k];
+    if (reset) memset(g_cnt, 0, sizeof(g_cnt));
+}
+
+static inline v2 V(float x, float y) { v2 r; r.x = x; r.y = y; return r; }
+static inline v2 vadd(v2 a, v2 b) { return V(a.x + b.x, a.y + b.y); }
+static inline v2 vsub(v2 a, v2 b) { return V(a.x - b.x, a.y - b.y); }
+static inline v2 vneg(v2 a) { return V(-a.x, -a.y); }
+static inline v2 smul(float s, v2 a) { return V(s * a.x, s * a.y); }
+static inline float dot(v2 a, v2 b) { return a.x * b.x + a.y * b.y; }
+static inline float crossvv(v2 a, v2 b) { return a.x * b.y - a.y * b.x; }
+static inline v2 crossvs(v2 a, float s) { return V(s * a.y, -s * a.x); }
+static inline v2 crosssv(float s, v2 a) { return V(-s * a.y, s * a.x); }
+static inline v2 rmul(rot q, v2 v) { return V(q.c * v.x - q.s * v.y, q.s * v.x + q.c * v.y); }
+static inline v2 rmult(rot q, v2 v) { return V(q.c * v.x + q.s * v.y, -q.s * v.x + q.c * v.y); }
+static inline v2 xmul(v2 p, rot q, v2 v) { return V((q.c * v.x - q.s * v.y) + p.x, (q.s * v.x + q.c * v.y) + p.y); }
+static inline v2 xmult(v2 p, rot q, v2 v)
+{
+    float px = v.x - p.x, py = v.y - p.y;
+    return V(q.c * px + q.s * py, -q.s * px + q.c * py);
+}
+static inline float vlen(v2 a) { return sqrtf(a.x * a.x + a.y * a.y); }
+static inline float vlen2(v2 a) { return a.x * a.x + a.y * a.y; }
+static inline float vdist2(v2 a, v2 b) { v2 c = vsub(a, b); return c.x * c.x + c.y * c.y; }
+static inline float b2min(float a, float b) { return a < b ? a : b; }
+static inline float b2max(float a, float b) { return a > b ? a : b; }
+static inline float b2clamp(float a, float lo, float hi) { return b2max(lo, b2min(a, hi)); }
+/* Box2D: b2Vec2::Normalize */
+static inline float vnormalize(v2* a)
+{
+    float l = vlen(*a);
+    if (l < FLT_EPSILON) return 0.0f;
+    float inv = 1.0f / l;
+    a->x *= inv;
+    a->y *= inv;
+    return l;
+}
+
+/* Shared deterministic sin/cos (stands in for libm sinf/cosf in b2Rot::Set,
+ * b2Mat22 angle setter): fdlibm-style Cody-Waite reduction + kernels in
+ * double, rounded once to float.  The HIP path carries the same code. */
+static void sincos_d(double x, double* so, double* co)
+{
+    const double invpio2 = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;
+    const double pio2_1t = 6.07710050650619224932e-11;
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double fn = floor(x * invpio2 + 0.5);
+    double y = (x - fn * pio2_1) - fn * pio2_1t;
+    long long n = (long long)fn;
+    double z = y * y;
+    double s = y + y * z * (S1 + z * (S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)))));
+    double c = 1.0 - 0.5 * z + z * z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    switch ((int)(n & 3)) {
+    case 0: *so = s; *co = c; break;
+    case 1: *so = c; *co = -s; break;
+    case 2: *so = -s; *co = -c; break;
+    default: *so = -c; *co = s; break;
+    }
+}
+
+void ora_sincos(float angle, float* s, float* c)
+{
+    double sd, cd;
+    sincos_d((double)angle, &sd, &cd);
+    *s = (float)sd;
+    *c = (float)cd;
+}
+
+static inline rot rot_of(float angle)
+{
+    rot q;
+    ora_sincos(angle, &q.s, &q.c);
+    return q;
+}
+
+/* simulation.py:20-23 from_polar: b2Mat22.angle = angle; R*b2Vec2(length, 0) */
+static inline v2 from_polar(float length, float angle)
+{
+    rot q = rot_of(angle);
+    return V(q.c * length + (-q.s) * 0.0f, q.s * length + q.c * 0.0f);
+}
+
+/* ------------------------------------------------------------------ */
+/* Shapes (Box2D b2PolygonShape / b2CircleShape)                        */
+/* ------------------------------------------------------------------ */
+/* Box2D: b2PolygonShape::SetAsBox(hx, hy) */
+void ora_poly_set_as_box(poly* p, float hx, float hy)
+{
+    p->count = 4;
+    p->v[0] = V(-hx, -hy);
+    p->v[1] = V(hx, -hy);
+    p->v[2] = V(hx, hy);
+    p->v[3] = V(-hx, hy);
+    p->n[0] = V(0.0f, -1.0f);
+    p->n[1] = V(1.0f, 0.0f);
+    p->n[2] = V(0.0f, 1.0f);
+    p->n[3] = V(-1.0f, 0.0f);
+}
+
+/* Box2D: b2PolygonShape::Set (weld, gift-wrap hull from the right-most
+ * point, normals by b2Vec2::Normalize).  Used by copy_shape
+ * (simulation.py:43-45) and by the camera cone (simulation.py:321-328). */
+void ora_poly_set(poly* p, const v2* verts, int count)
+{
+    v2 ps[8];
+    int n = count < 8 ? count : 8;
+    int tempCount = 0;
+    for (int i = 0; i < n; ++i) {
+        v2 v = verts[i];
+        int unique = 1;
+        for (int j = 0; j < tempCount; ++j) {
+            if (vdist2(v, ps[j]) < 0.5f * LINEAR_SLOP) { unique = 0; break; }
+        }
+        if (unique) ps[tempCount++] = v;
+    }
+    n = tempCount;
+    if (n < 3) { ora_poly_set_as_box(p, 1.0f, 1.0f); return; }
+    int i0 = 0;
+    float x0 = ps[0].x;
+    for (int i = 1; i < n; ++i) {
+        float x = ps[i].x;
+        if (x > x0 || (x == x0 && ps[i].y < ps[i0].y)) { i0 = i; x0 = x; }
+    }
+    int hull[8];
+    int m = 0;
+    int ih = i0;
+    for (;;) {
+        hull[m] = ih;
+        int ie = 0;
+        for (int j = 1; j < n; ++j) {
+            if (ie == ih) { ie = j; continue; }
+            v2 r = vsub(ps[ie], ps[hull[m]]);
+            v2 v = vsub(ps[j], ps[hull[m]]);
+            float c = crossvv(r, v);
+            if (c < 0.0f) ie = j;
+            if (c == 0.0f && vlen2(v) > vlen2(r)) ie = j;
+        }
+        ++m;
+        ih = ie;
+        if (ie == i0 || m >= 8) break;
+    }
+    if (m < 3) { ora_poly_set_as_box(p, 1.0f, 1.0f); return; }
+    p->count = m;
+    for (int i = 0; i < m; ++i) p->v[i] = ps[hull[i]];
+    for (int i = 0; i < m; ++i) {
+        int i2 = i + 1 < m ? i + 1 : 0;
+        v2 edge = vsub(p->v[i2], p->v[i]);
+        p->n[i] = crossvs(edge, 1.0f);
+        vnormalize(&p->n[i]);
+    }
+}
+
+/* Box2D: b2PolygonShape::TestPoint (skin radius ignored) */
+int32_t ora_poly_test_point(const poly* p, v2 xp, rot xq, v2 pt)
+{
+    v2 pLocal = rmult(xq, vsub(pt, xp));
+    for (int i = 0; i < p->count; ++i) {
+        float d = dot(p->n[i], vsub(pLocal, p->v[i]));
+        if (d > 0.0f) return 0;
+    }
+    return 1;
+}
+
+/* Box2D: b2CircleShape::TestPoint (centre = transform.p for m_p = 0) */
+int32_t ora_circle_test_point(float radius, v2 center, v2 pt)
+{
+    v2 d = vsub(pt, center);
+    return dot(d, d) <= radius * radius;
+}
+
+/* Box2D: b2CircleShape::RayCast */
+int32_t ora_ray_circle(float radius, v2 position, v2 p1, v2 p2, float maxf, float* fraction)
+{
+    v2 s = vsub(p1, position);
+    float b = dot(s, s) - radius * radius;
+    v2 r = vsub(p2, p1);
+    float c = dot(s, r);
+    float rr = dot(r, r);
+    float sigma = c * c - rr * b;
+    if (sigma < 0.0f || rr < FLT_EPSILON) return 0;
+    float a = -(c + sqrtf(sigma));
+    if (0.0f <= a && a <= maxf * rr) {
+        a /= rr;
+        *fraction = a;
+        return 1;
+    }
+    return 0;
+}
+
+/* Box2D: b2PolygonShape::RayCast */
+int32_t ora_ray_poly(const poly* p, v2 xp, rot xq, v2 p1w, v2 p2w, float maxf, float* fraction)
+{
+    v2 p1 = rmult(xq, vsub(p1w, xp));
+    v2 p2 = rmult(xq, vsub(p2w, xp));
+    v2 d = vsub(p2, p1);
+    float lower = 0.0f, upper = maxf;
+    int index = -1;
+    for (int i = 0; i < p->count; ++i) {
+        float numerator = dot(p->n[i], vsub(p->v[i], p1));
+        float denominator = dot(p->n[i], d);
+        if (denominator == 0.0f) {
+            if (numerator < 0.0f) return 0;
+        } else {
+            if (denominator < 0.0f && numerator < lower * denominator) {
+                lower = numerator / denominator;
+                index = i;
+            } else if (denominator > 0.0f && numerator < upper * denominator) {
+                upper = numerator / denominator;
+            }
+        }
+        if (upper < lower) return 0;
+    }
+    if (index >= 0) {
+        *fraction = lower;
+        return 1;
+    }
+    return 0;
+}
+
+/* Box2D: b2CircleShape::ComputeMass + b2Body::ResetMassData */
+void ora_body_mass(float radius, float density, float* inv_mass, float* inv_I)
+{
+    float mass = density * B2_PI * radius * radius;
+    float I = mass * (0.5f * radius * radius + 0.0f);
+    float m = 0.0f + mass;
+    float bI = 0.0f + I;
+    *inv_mass = 1.0f / m;
+    bI -= m * 0.0f;
+    *inv_I = 1.0f / bI;
+}
+
+/* ------------------------------------------------------------------ */
+/* Narrowphase                                                        */
+/* ------------------------------------------------------------------ */
+typedef struct { int touching; v2 ln, lp; } pc_man;
+
+/* Box2D: b2CollidePolygonAndCircle (polygon = fixture A, circle = B) */
+static pc_man collide_pc(const poly* P, v2 xp, rot xq, v2 c, float rP, float rC)
+{
+    pc_man m;
+    m.touching = 0;
+    m.ln = V(0, 0);
+    m.lp = V(0, 0);
+    v2 cLocal = xmult(xp, xq, c);
+    int normalIndex = 0;
+    float separation = -FLT_MAX;
+    float radius = rP + rC;
+    for (int i = 0; i < P->count; ++i) {
+        float s = dot(P->n[i], vsub(cLocal, P->v[i]));
+        if (s > radius) return m;
+        if (s > separation) { separation = s; normalIndex = i; }
+    }
+    int vi1 = normalIndex;
+    int vi2 = vi1 + 1 < P->count ? vi1 + 1 : 0;
+    v2 v1 = P->v[vi1], v2_ = P->v[vi2];
+    if (separation < FLT_EPSILON) {
+        m.touching = 1;
+        m.ln = P->n[normalIndex];
+        m.lp = smul(0.5f, vadd(v1, v2_));
+        return m;
+    }
+    float u1 = dot(vsub(cLocal, v1), vsub(v2_, v1));
+    float u2 = dot(vsub(cLocal, v2_), vsub(v1, v2_));
+    if (u1 <= 0.0f) {
+        if (vdist2(cLocal, v1) > radius * radius) return m;
+        m.touching = 1;
+        m.ln = vsub(cLocal, v1);
+        vnormalize(&m.ln);
+        m.lp = v1;
+    } else if (u2 <= 0.0f) {
+        if (vdist2(cLocal, v2_) > radius * radius) return m;
+        m.touching = 1;
+        m.ln = vsub(cLocal, v2_);
+        vnormalize(&m.ln);
+        m.lp = v2_;
+    } else {
+        v2 faceCenter = smul(0.5f, vadd(v1, v2_));
+        float sep = dot(vsub(cLocal, faceCenter), P->n[vi1]);
+        if (sep > radius) return m;
+        m.touching = 1;
+        m.ln = P->n[vi1];
+        m.lp = faceCenter;
+    }
+    return m;
+}
+
+/* Box2D: b2CollideCircles (touching test only; manifold is implicit) */
+static int collide_cc(v2 pA, v2 pB, float rA, float rB)
+{
+    v2 d = vsub(pB, pA);
+    float distSqr = dot(d, d);
+    float radius = rA + rB;
+    return !(distSqr > radius * radius);
+}
+
+/* ------------------------------------------------------------------ */
+/* Distance (GJK) + time of impact, polygon(A) vs circle(B)            */
+/* Box2D: b2Distance, b2SeparationFunction, b2TimeOfImpact             */
+/* ------------------------------------------------------------------ */
+typedef struct { v2 wA, wB, w; float a; int iA, iB; } svert;
+typedef struct { svert v[3]; int count; } simplex;
+typedef struct { float metric; int count; int iA[3], iB[3]; } scache;
+typedef struct { const v2* v; int count; float radius; } proxy;
+
+static int proxy_support(const proxy* p, v2 d)
+{
+    int best = 0;
+    float bv = dot(p->v[0], d);
+    for (int i = 1; i < p->count; ++i) {
+        float val = dot(p->v[i], d);
+        if (val > bv) { best = i; bv = val; }
+    }
+    return best;
+}
+
+static float simplex_metric(const simplex* s)
+{
+    switch (s->count) {
+    case 1: return 0.0f;
+    case 2: return vlen(vsub(s->v[0].w, s->v[1].w));
+    case 3: return crossvv(vsub(s->v[1].w, s->v[0].w), vsub(s->v[2].w, s->v[0].w));
+    default: return 0.0f;
+    }
+}
+
+static void simplex_read(simplex* s, const scache* cache, const proxy* pA, v2 xpA, rot xqA,
+                         const proxy* pB, v2 xpB, rot xqB)
+{
+    s->count = cache->count;
+    for (int i = 0; i < s->count; ++i) {
+        svert* v = &s->v[i];
+        v->iA = cache->iA[i];
+        v->iB = cache->iB[i];
+        v->wA = xmul(xpA, xqA, pA->v[v->iA]);
+        v->wB = xmul(xpB, xqB, pB->v[v->iB]);
+        v->w = vsub(v->wB, v->wA);
+        v->a = 0.0f;
+    }
+    if (s->count > 1) {
+        float metric1 = cache->metric;
+        float metric2 = simplex_metric(s);
+        if (metric2 < 0.5f * metric1 || 2.0f * metric1 < metric2 || metric2 < FLT_EPSILON) s->count = 0;
+    }
+    if (s->count == 0) {
+        svert* v = &s->v[0];
+        v->iA = 0;
+        v->iB = 0;
+        v->wA = xmul(xpA, xqA, pA->v[0]);
+        v->wB = xmul(xpB, xqB, pB->v[0]);
+        v->w = vsub(v->wB, v->wA);
+        v->a = 1.0f;
+        s->count = 1;
+    }
+}
+
+static void simplex_write(const simplex* s, scache* cache)
+{
+    cache->metric = simplex_metric(s);
+    cache->count = s->count;
+    for (int i = 0; i < s->count; ++i) {
+        cache->iA[i] = s->v[i].iA;
+        cache->iB[i] = s->v[i].iB;
+    }
+}
+
+static v2 simplex_search_dir(const simplex* s)
+{
+    if (s->count == 1) return vneg(s->v[0].w);
+    v2 e12 = vsub(s->v[1].w, s->v[0].w);
+    float sgn = crossvv(e12, vneg(s->v[0].w));
+    if (sgn > 0.0f) return crosssv(1.0f, e12);
+    return crossvs(e12, 1.0f);
+}
+
+static v2 simplex_closest(const simplex* s)
+{
+    switch (s->count) {
+    case 1: return s->v[0].w;
+    case 2: return vadd(smul(s->v[0].a, s->v[0].w), smul(s->v[1].a, s->v[1].w));
+    default: return V(0.0f, 0.0f);
+    }
+}
+
+static void simplex_witness(const simplex* s, v2* pA, v2* pB)
+{
+    switch (s->count) {
+    case 1: *pA = s->v[0].wA; *pB = s->v[0].wB; break;
+    case 2:
+        *pA = vadd(smul(s->v[0].a, s->v[0].wA), smul(s->v[1].a, s->v[1].wA));
+        *pB = vadd(smul(s->v[0].a, s->v[0].wB), smul(s->v[1].a, s->v[1].wB));
+        break;
+    case 3:
+        *pA = vadd(vadd(smul(s->v[0].a, s->v[0].wA), smul(s->v[1].a, s->v[1].wA)), smul(s->v[2].a, s->v[2].wA));
+        *pB = *pA;
+        break;
+    default: break;
+    }
+}
+
+static void simplex_solve2(simplex* s)
+{
+    v2 w1 = s->v[0].w, w2 = s->v[1].w;
+    v2 e12 = vsub(w2, w1);
+    float d12_2 = -dot(w1, e12);
+    if (d12_2 <= 0.0f) { s->v[0].a = 1.0f; s->count = 1; return; }
+    float d12_1 = dot(w2, e12);
+    if (d12_1 <= 0.0f) { s->v[1].a = 1.0f; s->count = 1; s->v[0] = s->v[1]; return; }
+    float inv = 1.0f / (d12_1 + d12_2);
+    s->v[0].a = d12_1 * inv;
+    s->v[1].a = d12_2 * inv;
+    s->count = 2;
+}
+
+static void simplex_solve3(simplex* s)
+{
+    v2 w1 = s->v[0].w, w2 = s->v[1].w, w3 = s->v[2].w;
+    v2 e12 = vsub(w2, w1);
+    float w1e12 = dot(w1, e12), w2e12 = dot(w2, e12);
+    float d12_1 = w2e12, d12_2 = -w1e12;
+    v2 e13 = vsub(w3, w1);
+    float w1e13 = dot(w1, e13), w3e13 = dot(w3, e13);
+    float d13_1 = w3e13, d13_2 = -w1e13;
+    v2 e23 = vsub(w3, w2);
+    float w2e23 = dot(w2, e23), w3e23 = dot(w3, e23);
+    float d23_1 = w3e23, d23_2 = -w2e23;
+    float n123 = crossvv(e12, e13);
+    float d123_1 = n123 * crossvv(w2, w3);
+    float d123_2 = n123 * crossvv(w3, w1);
+    float d123_3 = n123 * crossvv(w1, w2);
+    if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s->v[0].a = 1.0f; s->count = 1; return; }
+    if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) {
+        float inv = 1.0f / (d12_1 + d12_2);
+        s->v[0].a = d12_1 * inv; s->v[1].a = d12_2 * inv; s->count = 2; return;
+    }
+    if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) {
+        float inv = 1.0f / (d13_1 + d13_2);
+        s->v[0].a = d13_1 * inv; s->v[2].a = d13_2 * inv; s->count = 2; s->v[1] = s->v[2]; return;
+    }
+    if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s->v[1].a = 1.0f; s->count = 1; s->v[0] = s->v[1]; return; }
+    if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s->v[2].a = 1.0f; s->count = 1; s->v[0] = s->v[2]; return; }
+    if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) {
+        float inv = 1.0f / (d23_1 + d23_2);
+        s->v[1].a = d23_1 * inv; s->v[2].a = d23_2 * inv; s->count = 2; s->v[0] = s->v[2]; return;
+    }
+    float inv = 1.0f / (d123_1 + d123_2 + d123_3);
+    s->v[0].a = d123_1 * inv;
+    s->v[1].a = d123_2 * inv;
+    s->v[2].a = d123_3 * inv;
+    s->count = 3;
+}
+
+/* Box2D: b2Distance (useRadii = false); returns distance and witness pts */
+static float gjk_distance(scache* cache, const proxy* pA, v2 xpA, rot xqA, const proxy* pB, v2 xpB, rot xqB)
+{
+    simplex s;
+    simplex_read(&s, cache, pA, xpA, xqA, pB, xpB, xqB);
+    int saveA[3], saveB[3];
+    int iter = 0;
+    while (iter < 20) {
+        int saveCount = s.count;
+        for (int i = 0; i < saveCount; ++i) { saveA[i] = s.v[i].iA; saveB[i] = s.v[i].iB; }
+        if (s.count == 2) simplex_solve2(&s);
+        else if (s.count == 3) simplex_solve3(&s);
+        if (s.count == 3) break;
+        (void)simplex_closest(&s);
+        v2 d = simplex_search_dir(&s);
+        if (vlen2(d) < FLT_EPSILON * FLT_EPSILON) break;
+        svert* vx = &s.v[s.count];
+        vx->iA = proxy_support(pA, rmult(xqA, vneg(d)));
+        vx->wA = xmul(xpA, xqA, pA->v[vx->iA]);
+        vx->iB = proxy_support(pB, rmult(xqB, d));
+        vx->wB = xmul(xpB, xqB, pB->v[vx->iB]);
+        vx->w = vsub(vx->wB, vx->wA);
+        ++iter;
+        int dup = 0;
+        for (int i = 0; i < saveCount; ++i) {
+            if (vx->iA == saveA[i] && vx->iB == saveB[i]) { dup = 1; break; }
+        }
+        if (dup) break;
+        ++s.count;
+    }
+    v2 wpA = V(0.0f, 0.0f), wpB = V(0.0f, 0.0f);
+    simplex_witness(&s, &wpA, &wpB);
+    simplex_write(&s, cache);
+    return vlen(vsub(wpA, wpB));
+}
+
+typedef struct { v2 c0, c; float a0, a, alpha0; } sweep;
+
+/* Box2D: b2Sweep::GetTransform (localCenter = 0) */
+static void sweep_xf(const sweep* sw, float beta, int need_rot, v2* p, rot* q)
+{
+    *p = vadd(smul(1.0f - beta, sw->c0), smul(beta, sw->c));
+    if (need_rot) {
+        float angle = (1.0f - beta) * sw->a0 + beta * sw->a;
+        *q = rot_of(angle);
+    } else {
+        q->s = 0.0f;
+        q->c = 1.0f;
+    }
+}
+
+enum { SEP_POINTS = 0, SEP_FACEA = 1 };
+typedef struct {
+    const proxy *pA, *pB;
+    sweep sA, sB;
+    int type;
+    v2 lp, axis;
+} sepfn;
+
+static float sep_init(sepfn* f, const scache* cache, const proxy* pA, const sweep* sA, const proxy* pB,
+                      const sweep* sB, float t1)
+{
+    f->pA = pA;
+    f->pB = pB;
+    f->sA = *sA;
+    f->sB = *sB;
+    v2 xpA, xpB;
+    rot xqA, xqB;
+    sweep_xf(&f->sA, t1, 1, &xpA, &xqA);
+    sweep_xf(&f->sB, t1, 0, &xpB, &xqB);
+    if (cache->count == 1) {
+        f->type = SEP_POINTS;
+        v2 pa = xmul(xpA, xqA, pA->v[cache->iA[0]]);
+        v2 pb = xmul(xpB, xqB, pB->v[cache->iB[0]]);
+        f->axis = vsub(pb, pa);
+        return vnormalize(&f->axis);
+    }
+    /* two points on A (a single point on B cannot yield the faceB case) */
+    f->type = SEP_FACEA;
+    v2 a1 = pA->v[cache->iA[0]], a2 = pA->v[cache->iA[1]];
+    f->axis = crossvs(vsub(a2, a1), 1.0f);
+    vnormalize(&f->axis);
+    v2 normal = rmul(xqA, f->axis);
+    f->lp = smul(0.5f, vadd(a1, a2));
+    v2 pa = xmul(xpA, xqA, f->lp);
+    v2 pb = xmul(xpB, xqB, pB->v[cache->iB[0]]);
+    float s = dot(vsub(pb, pa), normal);
+    if (s < 0.0f) {
+        f->axis = vneg(f->axis);
+        s = -s;
+    }
+    return s;
+}
+
+static float sep_find_min(const sepfn* f, int* iA, int* iB, float t)
+{
+    v2 xpA, xpB;
+    rot xqA, xqB;
+    sweep_xf(&f->sA, t, 1, &xpA, &xqA);
+    sweep_xf(&f->sB, t, 0, &xpB, &xqB);
+    if (f->type == SEP_POINTS) {
+        v2 axisA = rmult(xqA, f->axis);
+        v2 axisB = rmult(xqB, vneg(f->axis));
+        *iA = proxy_support(f->pA, axisA);
+        *iB = proxy_support(f->pB, axisB);
+        v2 pa = xmul(xpA, xqA, f->pA->v[*iA]);
+        v2 pb = xmul(xpB, xqB, f->pB->v[*iB]);
+        return dot(vsub(pb, pa), f->axis);
+    }
+    v2 normal = rmul(xqA, f->axis);
+    v2 pa = xmul(xpA, xqA, f->lp);
+    v2 axisB = rmult(xqB, vneg(normal));
+    *iA = -1;
+    *iB = proxy_support(f->pB, axisB);
+    v2 pb = xmul(xpB, xqB, f->pB->v[*iB]);
+    return dot(vsub(pb, pa), normal);
+}
+
+static float sep_eval(const sepfn* f, int iA, int iB, float t)
+{
+    v2 xpA, xpB;
+    rot xqA, xqB;
+    sweep_xf(&f->sA, t, 1, &xpA, &xqA);
+    sweep_xf(&f->sB, t, 0, &xpB, &xqB);
+    if (f->type == SEP_POINTS) {
+        v2 pa = xmul(xpA, xqA, f->pA->v[iA]);
+        v2 pb = xmul(xpB, xqB, f->pB->v[iB]);
+        return dot(vsub(pb, pa), f->axis);
+    }
+    v2 normal = rmul(xqA, f->axis);
+    v2 pa = xmul(xpA, xqA, f->lp);
+    v2 pb = xmul(xpB, xqB, f->pB->v[iB]);
+    return dot(vsub(pb, pa), normal);
+}
+
+enum { TOI_UNKNOWN, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
+
+/* Box2D: b2TimeOfImpact (tMax = 1) */
+static int time_of_impact(const proxy* pA, sweep sA, const proxy* pB, sweep sB, float* tout)
+{
+    int state = TOI_UNKNOWN;
+    *tout = 1.0f;
+    /* b2Sweep::Normalize on the local copies */
+    {
+        float twoPi = 2.0f * B2_PI;
+        float d = twoPi * floorf(sA.a0 / twoPi);
+        sA.a0 -= d;
+        sA.a -= d;
+        d = twoPi * floorf(sB.a0 / twoPi);
+        sB.a0 -= d;
+        sB.a -= d;
+    }
+    float tMax = 1.0f;
+    float totalRadius = pA->radius + pB->radius;
+    float target = b2max(LINEAR_SLOP, totalRadius - 3.0f * LINEAR_SLOP);
+    float tolerance = 0.25f * LINEAR_SLOP;
+    float t1 = 0.0f;
+    int iter = 0;
+    scache cache;
+    cache.count = 0;
+    cache.metric = 0.0f;
+    for (;;) {
+        v2 xpA, xpB;
+        rot xqA, xqB;
+        sweep_xf(&sA, t1, 1, &xpA, &xqA);
+        sweep_xf(&sB, t1, 0, &xpB, &xqB);
+        float distance = gjk_distance(&cache, pA, xpA, xqA, pB, xpB, xqB);
+        if (distance <= 0.0f) { state = TOI_OVERLAPPED; *tout = 0.0f; break; }
+        if (distance < target + tolerance) { state = TOI_TOUCHING; *tout = t1; break; }
+        sepfn fcn;
+        sep_init(&fcn, &cache, pA, &sA, pB, &sB, t1);
+        int done = 0;
+        float t2 = tMax;
+        int pushBackIter = 0;
+        for (;;) {
+            int iA, iB;
+            float s2 = sep_find_min(&fcn, &iA, &iB, t2);
+            if (s2 > target + tolerance) { state = TOI_SEPARATED; *tout = tMax; done = 1; break; }
+            if (s2 > target - tolerance) { t1 = t2; break; }
+            float s1 = sep_eval(&fcn, iA, iB, t1);
+            if (s1 < target - tolerance) { state = TOI_FAILED; *tout = t1; done = 1; break; }
+            if (s1 <= target + tolerance) { state = TOI_TOUCHING; *tout = t1; done = 1; break; }
+            int rootIterCount = 0;
+            float a1 = t1, a2 = t2;
+            for (;;) {
+                float t;
+                if (rootIterCount & 1) t = a1 + (target - s1) * (a2 - a1) / (s2 - s1);
+                else t = 0.5f * (a1 + a2);
+                ++rootIterCount;
+                float s = sep_eval(&fcn, iA, iB, t);
+                if (fabsf(s - target) < tolerance) { t2 = t; break; }
+                if (s > target) { a1 = t; s1 = s; }
+                else { a2 = t; s2 = s; }
+                if (rootIterCount == 50) break;
+            }
+            ++pushBackIter;
+            if (pushBackIter == 8) break;
+        }
+        ++iter;
+        if (done) break;
+        if (iter == 20) { state = TOI_FAILED; *tout = t1; break; }
+    }
+    return state;
+}
+
+/* ------------------------------------------------------------------ */
+/* World step: Box2D b2World::Step = Collide -> Solve -> SolveTOI        */
+/* ------------------------------------------------------------------ */
+int32_t ora_world_sizeof(void) { return (int32_t)sizeof(ora_world); }
+
+typedef struct {
+    int type; /* 0 circles (agent i = A, agent j = B); 1 faceA (static s = A, agent i = B) */
+    int i, j; /* agents (j unused for faceA) */
+    int s;    /* static */
+    v2 ln, lp;
+    v2 normal, rA, rB;
+    float normalMass, tangentMass, ni, ti;
+} vcon;
+
+typedef struct {
+    v2 c0[ORA_MAX_DYN];
+    float a0[ORA_MAX_DYN];
+    pc_man man[ORA_MAX_DYN][ORA_MAX_STAT];
+    int man_fresh[ORA_MAX_DYN][ORA_MAX_STAT];
+} step_scratch;
+
+static inline void wake(ora_world* w, int i)
+{
+    if (!w->awake[i]) {
+        w->awake[i] = 1;
+        w->sleep_time[i] = 0.0f;
+    }
+}
+
+/* Box2D: b2Contact::Update for an agent-agent (circles) contact */
+static void update_aa(ora_world* w, int i, int j)
+{
+    ora_cmem* m = &w->aa[i][j];
+    int was = m->touching;
+    int touching = collide_cc(w->c[i], w->c[j], w->radius, w->radius);
+    if (touching) {
+        if (!was) { m->ni = 0.0f; m->ti = 0.0f; }
+    } else {
+        m->ni = 0.0f;
+        m->ti = 0.0f;
+    }
+    m->touching = touching;
+    if (touching != was) { wake(w, i); wake(w, j); }
+}
+
+/* Box2D: b2Contact::Update for a static polygon (A) - agent (B) contact */
+static int update_as(ora_world* w, step_scratch* sc, int i, int s)
+{
+    ora_cmem* m = &w->as[i][s];
+    int was = m->touching;
+    pc_man pm = collide_pc(&w->spoly[s], w->sp[s], w->sq[s], w->c[i], POLYGON_RADIUS, w->radius);
+    sc->man[i][s] = pm;
+    sc->man_fresh[i][s] = 1;
+    if (pm.touching) {
+        if (!was) { m->ni = 0.0f; m->ti = 0.0f; }
+    } else {
+        m->ni = 0.0f;
+        m->ti = 0.0f;
+    }
+    m->touching = pm.touching;
+    if (pm.touching != was) wake(w, i);
+    return pm.touching;
+}
+
+/* b2ContactSolver constructor + InitializeVelocityConstraints for one contact
+ * (positions/velocities read from the world arrays). */
+static void init_vcon(ora_world* w, vcon* k, float dtRatio, int warm)
+{
+    float mA, iA, mB, iB;
+    v2 cA, cB, vA, vB;
+    float wA, wB;
+    float rAd, rBd;
+    v2 point;
+    if (k->type == 0) {
+        mA = w->inv_mass; iA = w->inv_I; mB = w->inv_mass; iB = w->inv_I;
+        cA = w->c[k->i]; cB = w->c[k->j];
+        vA = w->v[k->i]; wA = w->w[k->i]; vB = w->v[k->j]; wB = w->w[k->j];
+        rAd = w->radius; rBd = w->radius;
+        /* b2WorldManifold::Initialize, e_circles */
+        v2 normal = V(1.0f, 0.0f);
+        v2 pointA = cA, pointB = cB;
+        if (vdist2(pointA, pointB) > FLT_EPSILON * FLT_EPSILON) {
+            normal = vsub(pointB, pointA);
+            vnormalize(&normal);
+        }
+        v2 wcA = vadd(pointA, smul(rAd, normal));
+        v2 wcB = vsub(pointB, smul(rBd, normal));
+        point = smul(0.5f, vadd(wcA, wcB));
+        k->normal = normal;
+    } else {
+        mA = 0.0f; iA = 0.0f; mB = w->inv_mass; iB = w->inv_I;
+        cA = w->sp[k->s]; cB = w->c[k->i];
+        vA = V(0.0f, 0.0f); wA = 0.0f; vB = w->v[k->i]; wB = w->w[k->i];
+        rAd = POLYGON_RADIUS; rBd = w->radius;
+        /* b2WorldManifold::Initialize, e_faceA */
+        rot qA = w->sq[k->s];
+        v2 normal = rmul(qA, k->ln);
+        v2 planePoint = xmul(cA, qA, k->lp);
+        v2 clipPoint = cB;
+        v2 wcA = vadd(clipPoint, smul(rAd - dot(vsub(clipPoint, planePoint), normal), normal));
+        v2 wcB = vsub(clipPoint, smul(rBd, normal));
+        point = smul(0.5f, vadd(wcA, wcB));
+        k->normal = normal;
+    }
+    (void)vA; (void)vB; (void)wA; (void)wB;
+    ora_cmem* mem = k->type == 0 ? &w->aa[k->i][k->j] : &w->as[k->i][k->s];
+    if (warm) {
+        k->ni = dtRatio * mem->ni;
+        k->ti = dtRatio * mem->ti;
+    } else {
+        k->ni = 0.0f;
+        k->ti = 0.0f;
+    }
+    k->rA = vsub(point, cA);
+    k->rB = vsub(point, cB);
+    float rnA = crossvv(k->rA, k->normal);
+    float rnB = crossvv(k->rB, k->normal);
+    float kNormal = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+    k->normalMass = kNormal > 0.0f ? 1.0f / kNormal : 0.0f;
+    v2 tangent = crossvs(k->normal, 1.0f);
+    float rtA = crossvv(k->rA, tangent);
+    float rtB = crossvv(k->rB, tangent);
+    float kTangent = mA + mB + iA * rtA * rtA + iB * rtB * rtB;
+    k->tangentMass = kTangent > 0.0f ? 1.0f / kTangent : 0.0f;
+    /* velocityBias = -restitution * vRel only when vRel < -1; restitution
+     * is 0 for every MaSurvival fixture (simulation.py:116-117) -> bias 0 */
+}
+
+/* accessors for a contact's two bodies' velocities (static: zero, massless) */
+static void vcon_bodies(ora_world* w, const vcon* k, float* mA, float* iA, float* mB, float* iB,
+                        v2** vA, float** wA, v2** vB, float** wB, v2* vzero, float* wzero)
+{
+    if (k->type == 0) {
+        *mA = w->inv_mass; *iA = w->inv_I; *vA = &w->v[k->i]; *wA = &w->w[k->i];
+        *mB = w->inv_mass; *iB = w->inv_I; *vB = &w->v[k->j]; *wB = &w->w[k->j];
+    } else {
+        *vzero = V(0.0f, 0.0f);
+        *wzero = 0.0f;
+        *mA = 0.0f; *iA = 0.0f; *vA = vzero; *wA = wzero;
+        *mB = w->inv_mass; *iB = w->inv_I; *vB = &w->v[k->i]; *wB = &w->w[k->i];
+    }
+}
+
+/* Box2D: b2ContactSolver::WarmStart */
+static void warm_start(ora_world* w, vcon* k)
+{
+    float mA, iA, mB, iB;
+    v2 *pvA, *pvB, vz;
+    float *pwA, *pwB, wz;
+    vcon_bodies(w, k, &mA, &iA, &mB, &iB, &pvA, &pwA, &pvB, &pwB, &vz, &wz);
+    v2 vA = *pvA, vB = *pvB;
+    float wA = *pwA, wB = *pwB;
+    v2 normal = k->normal;
+    v2 tangent = crossvs(normal, 1.0f);
+    v2 P = vadd(smul(k->ni, normal), smul(k->ti, tangent));
+    wA -= iA * crossvv(k->rA, P);
+    vA = vsub(vA, smul(mA, P));
+    wB += iB * crossvv(k->rB, P);
+    vB = vadd(vB, smul(mB, P));
+    if (k->type == 0) { *pvA = vA; *pwA = wA; }
+    *pvB = vB;
+    *pwB = wB;
+}
+
+/* Box2D: b2ContactSolver::SolveVelocityConstraints (1-point manifold) */
+static void solve_vcon(ora_world* w, vcon* k)
+{
+    float mA, iA, mB, iB;
+    v2 *pvA, *pvB, vz;
+    float *pwA, *pwB, wz;
+    vcon_bodies(w, k, &mA, &iA, &mB, &iB, &pvA, &pwA, &pvB, &pwB, &vz, &wz);
+    v2 vA = *pvA, vB = *pvB;
+    float wA = *pwA, wB = *pwB;
+    v2 normal = k->normal;
+    v2 tangent = crossvs(normal, 1.0f);
+    const float friction = 0.2f; /* b2MixFriction(0.2, 0.2) */
+    {
+        v2 dv = vsub(vsub(vadd(vB, crosssv(wB, k->rB)), vA), crosssv(wA, k->rA));
+        float vt = dot(dv, tangent) - 0.0f;
+        float lambda = k->tangentMass * (-vt);
+        float maxFriction = friction * k->ni;
+        float newImpulse = b2clamp(k->ti + lambda, -maxFriction, maxFriction);
+        lambda = newImpulse - k->ti;
+        k->ti = newImpulse;
+        v2 P = smul(lambda, tangent);
+        vA = vsub(vA, smul(mA, P));
+        wA -= iA * crossvv(k->rA, P);
+        vB = vadd(vB, smul(mB, P));
+        wB += iB * crossvv(k->rB, P);
+    }
+    {
+        v2 dv = vsub(vsub(vadd(vB, crosssv(wB, k->rB)), vA), crosssv(wA, k->rA));
+        float vn = dot(dv, normal);
+        float lambda = -k->normalMass * (vn - 0.0f);
+        float newImpulse = b2max(k->ni + lambda, 0.0f);
+        lambda = newImpulse - k->ni;
+        k->ni = newImpulse;
+        v2 P = smul(lambda, normal);
+        vA = vsub(vA, smul(mA, P));
+        wA -= iA * crossvv(k->rA, P);
+        vB = vadd(vB, smul(mB, P));
+        wB += iB * crossvv(k->rB, P);
+    }
+    if (k->type == 0) { *pvA = vA; *pwA = wA; }
+    *pvB = vB;
+    *pwB = wB;
+}
+
+/* Box2D: b2ContactSolver::SolvePositionConstraints / SolveTOIPositionConstraints
+ * for one contact; returns the separation it measured. */
+static float solve_pcon(ora_world* w, const vcon* k, float baumgarte)
+{
+    float mA, iA, mB, iB;
+    v2 cA, cB;
+    float aA, aB;
+    v2 normal, point;
+    float separation;
+    if (k->type == 0) {
+        mA = w->inv_mass; iA = w->inv_I; mB = w->inv_mass; iB = w->inv_I;
+        cA = w->c[k->i]; aA = w->a[k->i];
+        cB = w->c[k->j]; aB = w->a[k->j];
+        v2 pointA = cA, pointB = cB;
+        normal = vsub(pointB, pointA);
+        vnormalize(&normal);
+        point = smul(0.5f, vadd(pointA, pointB));
+        separation = dot(vsub(pointB, pointA), normal) - w->radius - w->radius;
+    } else {
+        mA = 0.0f; iA = 0.0f; mB = w->inv_mass; iB = w->inv_I;
+        cA = w->sp[k->s]; aA = w->sa[k->s];
+        cB = w->c[k->i]; aB = w->a[k->i];
+        rot qA = w->sq[k->s];
+        normal = rmul(qA, k->ln);
+        v2 planePoint = xmul(cA, qA, k->lp);
+        v2 clipPoint = cB;
+        separation = dot(vsub(clipPoint, planePoint), normal) - POLYGON_RADIUS - w->radius;
+        point = clipPoint;
+    }
+    v2 rA = vsub(point, cA);
+    v2 rB = vsub(point, cB);
+    float C = b2clamp(baumgarte * (separation + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
+    float rnA = crossvv(rA, normal);
+    float rnB = crossvv(rB, normal);
+    float K = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+    float impulse = K > 0.0f ? -C / K : 0.0f;
+    v2 P = smul(impulse, normal);
+    cA = vsub(cA, smul(mA, P));
+    aA -= iA * crossvv(rA, P);
+    cB = vadd(cB, smul(mB, P));
+    aB += iB * crossvv(rB, P);
+    if (k->type == 0) {
+        w->c[k->i] = cA; w->a[k->i] = aA;
+        w->c[k->j] = cB; w->a[k->j] = aB;
+    } else {
+        w->c[k->i] = cB; w->a[k->i] = aB;
+    }
+    return separation;
+}
+
+/* b2Island::Solve integration with the max translation / rotation clamp */
+static void integrate(ora_world* w, int i, float h)
+{
+    v2 v = w->v[i];
+    float wv = w->w[i];
+    v2 translation = smul(h, v);
+    if (dot(translation, translation) > MAX_TRANSLATION * MAX_TRANSLATION) {
+        float ratio = MAX_TRANSLATION / vlen(translation);
+        v.x *= ratio;
+        v.y *= ratio;
+    }
+    float rotation = h * wv;
+    if (rotation * rotation > MAX_ROTATION * MAX_ROTATION) {
+        float ratio = MAX_ROTATION / fabsf(rotation);
+        wv *= ratio;
+    }
+    w->c[i] = vadd(w->c[i], smul(h, v));
+    w->a[i] += h * wv;
+    w->v[i] = v;
+    w->w[i] = wv;
+}
+
+/* b2World::Solve + b2Island::Solve over every awake island */
+static void world_solve(ora_world* w, step_scratch* sc, float h, float dtRatio, int vel_iters, int pos_iters)
+{
+    int n = w->n_dyn;
+    int label[ORA_MAX_DYN];
+    for (int i = 0; i < n; ++i) label[i] = i;
+    /* islands: connected components over touching agent-agent contacts */
+    for (int pass = 0; pass < n; ++pass) {
+        int changed = 0;
+        for (int i = 0; i < n; ++i) {
+            if (!w->active[i]) continue;
+            for (int j = i + 1; j < n; ++j) {
+                if (!w->active[j] || !w->aa[i][j].touching) continue;
+                int l = label[i] < label[j] ? label[i] : label[j];
+                if (label[i] != l || label[j] != l) { label[i] = l; label[j] = l; changed = 1; }
+            }
+        }
+        if (!changed) break;
+    }
+    for (int root = 0; root < n; ++root) {
+        if (!w->active[root] || label[root] != root) continue;
+        int members[ORA_MAX_DYN], nm = 0, any_awake = 0;
+        for (int i = 0; i < n; ++i) {
+            if (w->active[i] && label[i] == root) {
+                members[nm++] = i;
+                any_awake |= w->awake[i];
+            }
+        }
+        if (!any_awake) continue;
+        for (int m = 0; m < nm; ++m) wake(w, members[m]);
+        /* contacts of this island in canonical order */
+        static __thread vcon ks[ORA_MAX_DYN * ORA_MAX_DYN + ORA_MAX_DYN * ORA_MAX_STAT];
+        int nk = 0;
+        for (int i = 0; i < n; ++i) {
+            if (!w->active[i] || label[i] != root) continue;
+            for (int j = i + 1; j < n; ++j) {
+                if (!w->active[j] || !w->aa[i][j].touching) continue;
+                vcon* k = &ks[nk++];
+                g_cnt[CNT_AA_CONTACT]++;
+                k->type = 0; k->i = i; k->j = j; k->s = -1;
+            }
+        }
+        for (int i = 0; i < n; ++i) {
+            if (!w->active[i] || label[i] != root) continue;
+            for (int s = 0; s < w->n_stat; ++s) {
+                if (!w->as[i][s].touching) continue;
+                if (!sc->man_fresh[i][s]) {
+                    /* not reachable with the canonical Collide order; keep a
+                     * fresh manifold rather than an undefined stale one */
+                    sc->man[i][s] = collide_pc(&w->spoly[s], w->sp[s], w->sq[s], w->c[i], POLYGON_RADIUS, w->radius);
+                    sc->man_fresh[i][s] = 1;
+                }
+                vcon* k = &ks[nk++];
+                k->type = 1; k->i = i; k->j = -1; k->s = s;
+                k->ln = sc->man[i][s].ln;
+                k->lp = sc->man[i][s].lp;
+            }
+        }
+        /* integrate velocities (damping, Pade form) */
+        for (int m = 0; m < nm; ++m) {
+            int i = members[m];
+            sc->c0[i] = w->c[i];
+            sc->a0[i] = w->a[i];
+            float ld = 1.0f / (1.0f + h * w->lin_damp);
+            w->v[i].x *= ld;
+            w->v[i].y *= ld;
+            float ad = 1.0f / (1.0f + h * w->ang_damp);
+            w->w[i] *= ad;
+        }
+        for (int q = 0; q < nk; ++q) init_vcon(w, &ks[q], dtRatio, 1);
+        for (int q = 0; q < nk; ++q) warm_start(w, &ks[q]);
+        for (int it = 0; it < vel_iters; ++it)
+            for (int q = 0; q < nk; ++q) solve_vcon(w, &ks[q]);
+        for (int q = 0; q < nk; ++q) {
+            ora_cmem* mem = ks[q].type == 0 ? &w->aa[ks[q].i][ks[q].j] : &w->as[ks[q].i][ks[q].s];
+            mem->ni = ks[q].ni;
+            mem->ti = ks[q].ti;
+        }
+        for (int m = 0; m < nm; ++m) integrate(w, members[m], h);
+        int positionSolved = 0;
+        for (int it = 0; it < pos_iters; ++it) {
+            float minSep = 0.0f;
+            for (int q = 0; q < nk; ++q) minSep = b2min(minSep, solve_pcon(w, &ks[q], BAUMGARTE));
+            if (minSep >= -3.0f * LINEAR_SLOP) { positionSolved = 1; break; }
+        }
+        /* sleep (b2Island::Solve, allowSleep) */
+        float minSleep = FLT_MAX;
+        const float linTolSqr = LINEAR_SLEEP_TOL * LINEAR_SLEEP_TOL;
+        const float angTolSqr = ANGULAR_SLEEP_TOL * ANGULAR_SLEEP_TOL;
+        for (int m = 0; m < nm; ++m) {
+            int i = members[m];
+            if (w->w[i] * w->w[i] > angTolSqr || dot(w->v[i], w->v[i]) > linTolSqr) {
+                w->sleep_time[i] = 0.0f;
+                minSleep = 0.0f;
+            } else {
+                w->sleep_time[i] += h;
+                minSleep = b2min(minSleep, w->sleep_time[i]);
+            }
+        }
+        if (minSleep >= TIME_TO_SLEEP && positionSolved) {
+            g_cnt[CNT_SLEEP]++;
+            for (int m = 0; m < nm; ++m) {
+                int i = members[m];
+                w->awake[i] = 0;
+                w->sleep_time[i] = 0.0f;
+                w->v[i] = V(0.0f, 0.0f);
+                w->w[i] = 0.0f;
+            }
+        }
+    }
+}
+
+/* b2World::SolveTOI restricted to one agent: agent-vs-static TOI events are
+ * independent across agents (statics never move; agent-agent pairs are
+ * excluded by Box2D's "two non-bullet dynamic bodies" rule). */
+static void world_toi_agent(ora_world* w, step_scratch* sc, int i, float dt, int vel_iters)
+{
+    sweep sw;
+    sw.c0 = sc->c0[i];
+    sw.a0 = sc->a0[i];
+    sw.c = w->c[i];
+    sw.a = w->a[i];
+    sw.alpha0 = 0.0f;
+    int valid[ORA_MAX_STAT], count[ORA_MAX_STAT], enabled[ORA_MAX_STAT];
+    float toi[ORA_MAX_STAT];
+    int ns = w->n_stat;
+    for (int s = 0; s < ns; ++s) { valid[s] = 0; count[s] = 0; enabled[s] = 1; toi[s] = 1.0f; }
+    v2 zero = V(0.0f, 0.0f);
+    proxy pB;
+    pB.v = &zero;
+    pB.count = 1;
+    pB.radius = w->radius;
+    for (;;) {
+        float minAlpha = 1.0f;
+        int minS = -1;
+        for (int s = 0; s < ns; ++s) {
+            if (!enabled[s]) continue;
+            if (count[s] > MAX_SUB_STEPS) continue;
+            float alpha;
+            if (valid[s]) {
+                alpha = toi[s];
+            } else {
+                float alpha0 = sw.alpha0;
+                proxy pA;
+                pA.v = w->spoly[s].v;
+                pA.count = w->spoly[s].count;
+                pA.radius = POLYGON_RADIUS;
+                sweep sA;
+                sA.c0 = w->sp[s];
+                sA.c = w->sp[s];
+                sA.a0 = w->sa[s];
+                sA.a = w->sa[s];
+                sA.alpha0 = alpha0;
+                float beta;
+                int st = time_of_impact(&pA, sA, &pB, sw, &beta);
+                if (st == TOI_TOUCHING) alpha = b2min(alpha0 + (1.0f - alpha0) * beta, 1.0f);
+                else alpha = 1.0f;
+                toi[s] = alpha;
+                valid[s] = 1;
+            }
+            if (alpha < minAlpha) { minAlpha = alpha; minS = s; }
+        }
+        if (minS < 0 || 1.0f - 10.0f * FLT_EPSILON < minAlpha) break;
+        sweep backup = sw;
+        /* b2Body::Advance */
+        {
+            float beta = (minAlpha - sw.alpha0) / (1.0f - sw.alpha0);
+            sw.c0 = vadd(sw.c0, smul(beta, vsub(sw.c, sw.c0)));
+            sw.a0 += beta * (sw.a - sw.a0);
+            sw.alpha0 = minAlpha;
+            sw.c = sw.c0;
+            sw.a = sw.a0;
+        }
+        w->c[i] = sw.c;
+        w->a[i] = sw.a;
+        int touching = update_as(w, sc, i, minS);
+        valid[minS] = 0;
+        ++count[minS];
+        if (!touching) {
+            g_cnt[CNT_TOI_RESTORE]++;
+            enabled[minS] = 0;
+            sw = backup;
+            w->c[i] = sw.c;
+            w->a[i] = sw.a;
+            continue;
+        }
+        g_cnt[CNT_TOI_EVENT]++;
+        wake(w, i);
+        /* TOI island: the min contact, then the agent's other touching static contacts */
+        int isl[ORA_MAX_STAT], ni = 0;
+        isl[ni++] = minS;
+        for (int s = 0; s < ns; ++s) {
+            if (s == minS) continue;
+            enabled[s] = 1; /* b2Contact::Update re-enables every updated contact */
+            if (update_as(w, sc, i, s)) isl[ni++] = s;
+        }
+        /* b2Island::SolveTOI */
+        vcon ks[ORA_MAX_STAT];
+        for (int q = 0; q < ni; ++q) {
+            ks[q].type = 1; ks[q].i = i; ks[q].j = -1; ks[q].s = isl[q];
+            ks[q].ln = sc->man[i][isl[q]].ln;
+            ks[q].lp = sc->man[i][isl[q]].lp;
+        }
+        for (int it = 0; it < 20; ++it) {
+            float minSep = 0.0f;
+            for (int q = 0; q < ni; ++q) minSep = b2min(minSep, solve_pcon(w, &ks[q], TOI_BAUMGARTE));
+            if (minSep >= -1.5f * LINEAR_SLOP) break;
+        }
+        sw.c0 = w->c[i];
+        sw.a0 = w->a[i];
+        for (int q = 0; q < ni; ++q) init_vcon(w, &ks[q], 1.0f, 0);
+        for (int it = 0; it < vel_iters; ++it)
+            for (int q = 0; q < ni; ++q) solve_vcon(w, &ks[q]);
+        float h = (1.0f - minAlpha) * dt;
+        integrate(w, i, h);
+        sw.c = w->c[i];
+        sw.a = w->a[i];
+        for (int s = 0; s < ns; ++s) valid[s] = 0;
+    }
+    w->c[i] = sw.c;
+    w->a[i] = sw.a;
+}
+
+void ora_world_step(ora_world* w, float dt, int32_t vel_iters, int32_t pos_iters)
+{
+    static __thread step_scratch sc;
+    memset(sc.man_fresh, 0, sizeof(sc.man_fresh));
+    int n = w->n_dyn;
+    float inv_dt = dt > 0.0f ? 1.0f / dt : 0.0f;
+    float dtRatio = w->inv_dt0 * dt;
+    /* Collide (canonical order: agent-agent pairs, then agent-static) */
+    for (int i = 0; i < n; ++i) {
+        if (!w->active[i]) continue;
+        for (int j = i + 1; j < n; ++j) {
+            if (!w->active[j]) continue;
+            if (!(w->awake[i] || w->awake[j])) continue;
+            update_aa(w, i, j);
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        if (!w->active[i] || !w->awake[i]) continue;
+        for (int s = 0; s < w->n_stat; ++s) update_as(w, &sc, i, s);
+    }
+    world_solve(w, &sc, dt, dtRatio, vel_iters, pos_iters);
+    for (int i = 0; i < n; ++i) {
+        if (!w->active[i] || !w->awake[i]) continue;
+        world_toi_agent(w, &sc, i, dt, vel_iters);
+    }
+    w->inv_dt0 = inv_dt;
+}
+
+/* ------------------------------------------------------------------ */
+/* numpy Generator(PCG64)                                              */
+/* ------------------------------------------------------------------ */
+typedef unsigned __int128 u128;
+
+uint64_t ora_pcg64_next64(ora_pcg64* r)
+{
+    u128 st = ((u128)r->st_hi << 64) | r->st_lo;
+    u128 inc = ((u128)r->inc_hi << 64) | r->inc_lo;
+    const u128 mult = ((u128)0x2360ED051FC65DA4ULL << 64) | 0x4385DF649FCCF645ULL;
+    st = st * mult + inc;
+    r->st_hi = (uint64_t)(st >> 64);
+    r->st_lo = (uint64_t)st;
+    uint64_t xored = r->st_hi ^ r->st_lo;
+    unsigned rot = (unsigned)(r->st_hi >> 58);
+    return (xored >> rot) | (xored << ((64u - rot) & 63u));
+}
+
+uint32_t ora_pcg64_next32(ora_pcg64* r)
+{
+    if (r->has_uint32) {
+        r->has_uint32 = 0;
+        return r->uinteger;
+    }
+    uint64_t next = ora_pcg64_next64(r);
+    r->has_uint32 = 1;
+    r->uinteger = (uint32_t)(next >> 32);
+    return (uint32_t)(next & 0xffffffffULL);
+}
+
+double ora_pcg64_random(ora_pcg64* r) { return (double)(ora_pcg64_next64(r) >> 11) * (1.0 / 9007199254740992.0); }
+
+/* numpy random_interval (used by Generator.shuffle) */
+uint64_t ora_random_interval(ora_pcg64* r, uint64_t max)
+{
+    if (max == 0) return 0;
+    uint64_t mask = max, value;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    mask |= mask >> 32;
+    if (max <= 0xffffffffULL) {
+        while ((value = (ora_pcg64_next32(r) & mask)) > max) {}
+    } else {
+        while ((value = (ora_pcg64_next64(r) & mask)) > max) {}
+    }
+    return value;
+}
+
+/* numpy random_standard_normal (ziggurat) */
+double ora_standard_normal(ora_pcg64* r)
+{
+    for (;;) {
+        uint64_t rr = ora_pcg64_next64(r);
+        int idx = (int)(rr & 0xff);
+        rr >>= 8;
+        int sign = (int)(rr & 0x1);
+        uint64_t rabs = (rr >> 1) & 0x000fffffffffffffULL;
+        double x = (double)rabs * mas_wi_double[idx];
+        if (sign & 0x1) x = -x;
+        if (rabs < mas_ki_double[idx]) return x;
+        if (idx == 0) {
+            for (;;) {
+                double xx = -MAS_ZIGGURAT_NOR_INV_R * log1p(-ora_pcg64_random(r));
+                double yy = -log1p(-ora_pcg64_random(r));
+                if (yy + yy > xx * xx)
+                    return ((rabs >> 8) & 0x1) ? -(MAS_ZIGGURAT_NOR_R + xx) : MAS_ZIGGURAT_NOR_R + xx;
+            }
+        } else {
+            if (((mas_fi_double[idx - 1] - mas_fi_double[idx]) * ora_pcg64_random(r) + mas_fi_double[idx]) <
+                exp(-0.5 * x * x))
+                return x;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Env (reference semantics.py / simulation.py / masurvival_env.py)     */
+/* ------------------------------------------------------------------ */
+#define OA ORA_MAX_DYN
+#define OB 64
+#define OH 64
+#define NWALLS 4
+
+enum { K_BOX = 0, K_BITEM = 1, K_HEAL = 2, K_WALL = 3, K_AGENT = 4 };
+enum { IT_NONE = 0, IT_HEAL = 1, IT_BOX = 2 };
+/* damage causes (Health.causes values) */
+#define CAUSE_NONE (-1)
+#define CAUSE_BADGE0 1000
+#define CAUSE_ZONE 2000
+
+typedef struct { int kind; poly shape; int owner; } item;
+typedef struct { uint32_t serial; v2 pos; } heal_t;
+typedef struct { uint32_t serial; v2 pos; poly shape; int owner; } bitem_t;
+typedef struct { uint32_t serial; v2 pos; float angle; rot q; poly shape; int health; int hinit; int vuln; int cause; } box_t;
+typedef struct { v2 pos; poly shape; int owner; } pend_t;
+
+struct ora_env {
+    mas_config cfg;
+    int A, H, B, D, as_;
+    int melee_cd;
+    ora_pcg64 rng;
+    ora_world w;
+    float agent_r, heal_r, bitem_r;
+    /* agents (slot = IndexBodies id) */
+    int alive[OA];
+    uint32_t aserial[OA];
+    int health[OA];
+    int cause[OA];
+    int cooldown[OA];
+    int inv_n[OA];
+    item inv[OA][ORA_MAX_SLOTS];
+    /* groups in list order */
+    int nbox;
+    box_t box[OB];
+    int nbi;
+    bitem_t bi[OB];
+    int nheal;
+    heal_t heal[OH];
+    int npend;
+    pend_t pend[OB];
+    poly wall_poly;
+    v2 wall_pos[NWALLS];
+    float wall_angle[NWALLS];
+    rot wall_q[NWALLS];
+    uint32_t wall_serial[NWALLS];
+    /* safe zone */
+    v2 zcent[MAS_MAX_ZONE_PHASES + 1];
+    double zrad[MAS_MAX_ZONE_PHASES + 1];
+    int phase, t_cooldown, t_shrink, endgame;
+    v2 zpos;
+    float zradius;
+    /* cameras: seen[list position] = serials */
+    poly cone;
+    int cam_n;
+    int seen_n[OA];
+    uint32_t seen[OA][4 * OB + OH + OA + NWALLS];
+    /* per-step buffers */
+    int ndeaths;
+    int deaths[OA];
+    int nkills;
+    int kills_cause[OA];
+    int uses_heal, uses_box;
+    int last_kills[OA];
+    float last_rewards[OA];
+    int steps;
+    uint32_t next_serial;
+    float stats[MAS_STATS_WIDTH];
+    int stats_init;
+    /* grid */
+    int ngrid;
+    v2 grid[4096];
+};
+
+static int team_of(const ora_env* e, int id) { return id < e->A / 2 ? 0 : 1; }
+
+int32_t ora_env_obs_dim(const ora_env* e) { return e->D; }
+
+ora_env* ora_env_create(const mas_config* cfg, char* err, int32_t errlen)
+{
+    if (cfg->n_agents < 2 || cfg->n_agents > OA || cfg->n_heals < 0 || cfg->n_heals > OH || cfg->n_boxes < 0 ||
+        cfg->n_boxes > OB || cfg->slots < 0 || cfg->slots > ORA_MAX_SLOTS || cfg->zone_phases < 1 ||
+        cfg->zone_phases > MAS_MAX_ZONE_PHASES || cfg->grid_size * cfg->grid_size > 4096) {
+        if (err) snprintf(err, errlen, "oracle: unsupported config sizes");
+        return NULL;
+    }
+    if (cfg->n_agents + cfg->n_heals + cfg->n_boxes > cfg->grid_size * cfg->grid_size) {
+        if (err) snprintf(err, errlen, "oracle: more spawns than grid cells (IndexError semantics.py:77)");
+        return NULL;
+    }
+    ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
+    e->cfg = *cfg;
+    e->A = cfg->n_agents;
+    e->H = cfg->n_heals;
+    e->B = cfg->n_boxes;
+    e->as_ = 8 + (cfg->teams ? 1 : 0);
+    e->melee_cd = cfg->melee_cooldown;
+    int A = e->A, H = e->H, B = e->B;
+    e->D = e->as_ * A + 6 + (A - 1) + (H > 0 ? 3 * H + 2 : 0) + (B > 0 ? 23 * B + 9 : 0);
+    e->agent_r = (float)(cfg->agent_size / 2.0);
+    e->heal_r = (float)(cfg->heal_size / 2.0);
+    e->bitem_r = (float)(cfg->box_item_size / 2.0);
+    /* world constants */
+    e->w.n_dyn = A;
+    e->w.radius = e->agent_r;
+    ora_body_mass(e->agent_r, 1.0f, &e->w.inv_mass, &e->w.inv_I);
+    e->w.lin_damp = 0.8f; /* simulation.py:114 default_damping */
+    e->w.ang_damp = 0.8f;
+    /* ThickRoomWalls (semantics.py:685-695) */
+    double height = cfg->floor_size;
+    double width = height / cfg->wall_aspect_ratio;
+    ora_poly_set_as_box(&e->wall_poly, (float)(width / 2.0), (float)(height / 2.0));
+    double off = cfg->floor_size / 2.0;
+    e->wall_pos[0] = V((float)(-off), 0.0f);
+    e->wall_angle[0] = 0.0f;
+    e->wall_pos[1] = V(0.0f, (float)off);
+    e->wall_angle[1] = (float)(M_PI / 2.0);
+    e->wall_pos[2] = V((float)off, 0.0f);
+    e->wall_angle[2] = 0.0f;
+    e->wall_pos[3] = V(0.0f, (float)(-off));
+    e->wall_angle[3] = (float)(M_PI / 2.0);
+    for (int k = 0; k < NWALLS; ++k) e->wall_q[k] = rot_of(e->wall_angle[k]);
+    /* Cameras vision cone (simulation.py:321-328) */
+    {
+        v2 left = from_polar(cfg->cam_depth, (float)(cfg->cam_fov / 2.0));
+        v2 center = V(cfg->cam_depth, 0.0f);
+        v2 right = from_polar(cfg->cam_depth, (float)(-cfg->cam_fov / 2.0));
+        v2 vs[4] = {V(0.0f, 0.0f), left, center, right};
+        ora_poly_set(&e->cone, vs, 4);
+    }
+    /* square_grid (semantics.py:987-992), float64 then b2Vec2 */
+    int g = cfg->grid_size;
+    e->ngrid = g * g;
+    for (int k = 0; k < g * g; ++k) {
+        int ii = k % g, jj = k / g;
+        double ci = (double)ii / g + 0.5 / g;
+        double cj = (double)jj / g + 0.5 / g;
+        ci = cfg->floor_size * ci - cfg->floor_size / 2.0;
+        cj = cfg->floor_size * cj - cfg->floor_size / 2.0;
+        e->grid[k] = V((float)ci, (float)cj);
+    }
+    return e;
+}
+
+void ora_env_destroy(ora_env* e) { free(e); }
+
+void ora_env_set_rng(ora_env* e, const uint64_t* st6)
+{
+    e->rng.st_hi = st6[0];
+    e->rng.st_lo = st6[1];
+    e->rng.inc_hi = st6[2];
+    e->rng.inc_lo = st6[3];
+    e->rng.has_uint32 = (int32_t)st6[4];
+    e->rng.uinteger = (uint32_t)st6[5];
+}
+
+void ora_env_get_rng(const ora_env* e, uint64_t* st6)
+{
+    st6[0] = e->rng.st_hi;
+    st6[1] = e->rng.st_lo;
+    st6[2] = e->rng.inc_hi;
+    st6[3] = e->rng.inc_lo;
+    st6[4] = (uint64_t)e->rng.has_uint32;
+    st6[5] = e->rng.uinteger;
+}
+
+/* ---- world static slots: walls 0..3, then boxes in list order ---- */
+static void sync_statics(ora_env* e)
+{
+    ora_world* w = &e->w;
+    w->n_stat = NWALLS + e->nbox;
+    for (int k = 0; k < NWALLS; ++k) {
+        w->sp[k] = e->wall_pos[k];
+        w->sa[k] = e->wall_angle[k];
+        w->sq[k] = e->wall_q[k];
+        w->spoly[k] = e->wall_poly;
+    }
+    for (int b = 0; b < e->nbox; ++b) {
+        w->sp[NWALLS + b] = e->box[b].pos;
+        w->sa[NWALLS + b] = e->box[b].angle;
+        w->sq[NWALLS + b] = e->box[b].q;
+        w->spoly[NWALLS + b] = e->box[b].shape;
+    }
+}
+
+/* Group.spawn for boxes (simulation.py:178-183): appended, new contacts */
+static void spawn_box(ora_env* e, v2 pos, const poly* shape, int vuln)
+{
+    box_t* b = &e->box[e->nbox];
+    b->serial = e->next_serial++;
+    b->pos = pos;
+    b->angle = 0.0f;
+    b->q = rot_of(0.0f);
+    b->shape = *shape;
+    b->health = 0;
+    b->hinit = 0;
+    b->vuln = vuln;
+    b->cause = CAUSE_NONE;
+    for (int i = 0; i < e->A; ++i) {
+        e->w.as[i][NWALLS + e->nbox].touching = 0;
+        e->w.as[i][NWALLS + e->nbox].ni = 0.0f;
+        e->w.as[i][NWALLS + e->nbox].ti = 0.0f;
+    }
+    e->nbox++;
+    sync_statics(e);
+}
+
+static void despawn_box(ora_env* e, int idx)
+{
+    for (int b = idx; b + 1 < e->nbox; ++b) {
+        e->box[b] = e->box[b + 1];
+        for (int i = 0; i < e->A; ++i) e->w.as[i][NWALLS + b] = e->w.as[i][NWALLS + b + 1];
+    }
+    e->nbox--;
+    sync_statics(e);
+}
+
+static void spawn_heal(ora_env* e, v2 pos)
+{
+    if (e->nheal >= OH) return;
+    e->heal[e->nheal].serial = e->next_serial++;
+    e->heal[e->nheal].pos = pos;
+    e->nheal++;
+}
+
+static void spawn_bitem(ora_env* e, v2 pos, const poly* shape, int owner)
+{
+    if (e->nbi >= OB) return;
+    bitem_t* b = &e->bi[e->nbi++];
+    b->serial = e->next_serial++;
+    b->pos = pos;
+    b->shape = *shape;
+    b->owner = owner;
+}
+
+/* Health._change_health (semantics.py:490-500) for agents */
+static void agent_change_health(ora_env* e, int i, int delta, int cause)
+{
+    if (!e->alive[i]) return;
+    if (e->cfg.teams && cause == CAUSE_BADGE0 + team_of(e, i)) return; /* immunities (TwoTeams :942-946) */
+    e->health[i] += delta;
+    e->cause[i] = cause;
+}
+
+static void box_change_health(ora_env* e, int b, int delta, int cause)
+{
+    box_t* bx = &e->box[b];
+    if (!bx->hinit) return; /* body not in healths yet */
+    if (bx->vuln != CAUSE_NONE && cause != bx->vuln) return; /* vulnerabilities (OwnedObjectItem :883-884) */
+    bx->health += delta;
+    bx->cause = cause;
+}
+
+/* ---- fixture iteration in canonical order (groups in dict order) ---- */
+typedef struct { int kind, idx; } bref;
+
+/* simulation.py:431-439 laser_scan + LaserRayCastCallback (:471-484) */
+static bref ray_cast(const ora_env* e, v2 p1, v2 p2)
+{
+    bref hit = {-1, -1};
+    float maxf = 1.0f, f;
+    for (int b = 0; b < e->nbox; ++b) {
+        if (ora_ray_poly(&e->box[b].shape, e->box[b].pos, e->box[b].q, p1, p2, maxf, &f)) {
+            hit.kind = K_BOX; hit.idx = b; maxf = f;
+            if (maxf == 0.0f) return hit;
+        }
+    }
+    for (int b = 0; b < e->nbi; ++b) {
+        if (ora_ray_circle(e->bitem_r, e->bi[b].pos, p1, p2, maxf, &f)) {
+            hit.kind = K_BITEM; hit.idx = b; maxf = f;
+            if (maxf == 0.0f) return hit;
+        }
+    }
+    for (int h = 0; h < e->nheal; ++h) {
+        if (ora_ray_circle(e->heal_r, e->heal[h].pos, p1, p2, maxf, &f)) {
+            hit.kind = K_HEAL; hit.idx = h; maxf = f;
+            if (maxf == 0.0f) return hit;
+        }
+    }
+    for (int k = 0; k < NWALLS; ++k) {
+        if (ora_ray_poly(&e->wall_poly, e->wall_pos[k], e->wall_q[k], p1, p2, maxf, &f)) {
+            hit.kind = K_WALL; hit.idx = k; maxf = f;
+            if (maxf == 0.0f) return hit;
+        }
+    }
+    for (int i = 0; i < e->A; ++i) {
+        if (!e->alive[i]) continue;
+        if (ora_ray_circle(e->agent_r, e->w.c[i], p1, p2, maxf, &f)) {
+            hit.kind = K_AGENT; hit.idx = i; maxf = f;
+            if (maxf == 0.0f) return hit;
+        }
+    }
+    return hit;
+}
+
+static v2 body_pos(const ora_env* e, bref r)
+{
+    switch (r.kind) {
+    case K_BOX: return e->box[r.idx].pos;
+    case K_BITEM: return e->bi[r.idx].pos;
+    case K_HEAL: return e->heal[r.idx].pos;
+    case K_WALL: return e->wall_pos[r.idx];
+    default: return e->w.c[r.idx];
+    }
+}
+
+static uint32_t body_serial(const ora_env* e, bref r)
+{
+    switch (r.kind) {
+    case K_BOX: return e->box[r.idx].serial;
+    case K_BITEM: return e->bi[r.idx].serial;
+    case K_HEAL: return e->heal[r.idx].serial;
+    case K_WALL: return e->wall_serial[r.idx];
+    default: return e->aserial[r.idx];
+    }
+}
+
+/* all bodies in canonical order */
+static int all_bodies(const ora_env* e, bref* out)
+{
+    int n = 0;
+    for (int b = 0; b < e->nbox; ++b) { out[n].kind = K_BOX; out[n].idx = b; ++n; }
+    for (int b = 0; b < e->nbi; ++b) { out[n].kind = K_BITEM; out[n].idx = b; ++n; }
+    for (int h = 0; h < e->nheal; ++h) { out[n].kind = K_HEAL; out[n].idx = h; ++n; }
+    for (int k = 0; k < NWALLS; ++k) { out[n].kind = K_WALL; out[n].idx = k; ++n; }
+    for (int i = 0; i < e->A; ++i) {
+        if (!e->alive[i]) continue;
+        out[n].kind = K_AGENT; out[n].idx = i; ++n;
+    }
+    return n;
+}
+
+/* Cameras._update_seen (simulation.py:336-354) over the alive agents list */
+static void update_seen(ora_env* e)
+{
+    bref bodies[4 * OB + OH + OA + NWALLS];
+    int nb = all_bodies(e, bodies);
+    e->cam_n = 0;
+    for (int i = 0; i < e->A; ++i) {
+        if (!e->alive[i]) continue;
+        int p = e->cam_n++;
+        e->seen_n[p] = 0;
+        v2 pos = e->w.c[i];
+        rot q = rot_of(e->w.a[i]);
+        for (int k = 0; k < nb; ++k) {
+            v2 oc = body_pos(e, bodies[k]);
+            if (!ora_poly_test_point(&e->cone, pos, q, oc)) continue;
+            if (bodies[k].kind == K_AGENT && bodies[k].idx == i) continue;
+            v2 d = vsub(oc, pos);
+            v2 end = vadd(pos, smul((float)(1.0 + 1e-6), d));
+            bref hit = ray_cast(e, pos, end);
+            if (hit.kind < 0) continue;
+            if (hit.kind == bodies[k].kind && hit.idx == bodies[k].idx) e->seen[p][e->seen_n[p]++] = body_serial(e, hit);
+        }
+    }
+}
+
+static int seen_has(const ora_env* e, int p, uint32_t serial)
+{
+    for (int k = 0; k < e->seen_n[p]; ++k)
+        if (e->seen[p][k] == serial) return 1;
+    return 0;
+}
+
+/* ---- observations: fetch_observations (masurvival_env.py:510-657) ---- */
+static void write_obs(ora_env* e, float* obs)
+{
+    int A = e->A, H = e->H, B = e->B, D = e->D, as_ = e->as_;
+    memset(obs, 0, sizeof(float) * (size_t)A * (size_t)D);
+    /* key offsets in sorted-key order */
+    int off = 0;
+    int o_agent = off; off += as_;
+    int o_bi = -1, o_bim = -1, o_bs = -1, o_bsm = -1, o_box = -1, o_boxm = -1;
+    int o_hs = -1, o_hsm = -1, o_heal = -1, o_healm = -1;
+    if (B > 0) {
+        o_bi = off; off += 10 * B;
+        o_bim = off; off += B;
+        o_bs = off; off += 8;
+        o_bsm = off; off += 1;
+        o_box = off; off += 11 * B;
+        o_boxm = off; off += B;
+    }
+    if (H > 0) {
+        o_hs = off; off += 1;
+        o_hsm = off; off += 1;
+        o_heal = off; off += 2 * H;
+        o_healm = off; off += H;
+    }
+    int o_oth = off; off += (A - 1) * as_;
+    int o_othm = off; off += A - 1;
+    int o_zone = off; off += 6;
+    /* agent rows (_fetch_agents_observations :659-704) */
+    float arow[OA][9];
+    int post_pos[OA];
+    int np = 0;
+    for (int i = 0; i < A; ++i) post_pos[i] = e->alive[i] ? np++ : -1;
+    for (int i = 0; i < A; ++i) {
+        int k = 0;
+        arow[i][k++] = (float)i;
+        if (e->cfg.teams) arow[i][k++] = (float)team_of(e, i);
+        if (e->alive[i]) {
+            arow[i][k++] = (float)e->health[i];
+            arow[i][k++] = e->w.c[i].x;
+            arow[i][k++] = e->w.c[i].y;
+            arow[i][k++] = e->w.a[i];
+            arow[i][k++] = e->w.v[i].x;
+            arow[i][k++] = e->w.v[i].y;
+            arow[i][k++] = e->w.w[i];
+        } else {
+            for (int z = 0; z < 7; ++z) arow[i][k++] = 0.0f;
+        }
+    }
+    for (int i = 0; i < A; ++i) {
+        float* row = obs + (size_t)i * D;
+        for (int k = 0; k < as_; ++k) row[o_agent + k] = arow[i][k];
+        int q = 0;
+        for (int j = 0; j < A; ++j) {
+            if (j == i) continue;
+            for (int k = 0; k < as_; ++k) row[o_oth + q * as_ + k] = arow[j][k];
+            /* others_mask: seen list at the post-despawn list index (quirk D1) */
+            float m = 1.0f;
+            if (e->alive[i] && e->alive[j]) {
+                int p = post_pos[i];
+                if (p < e->cam_n && seen_has(e, p, e->aserial[j])) m = 0.0f;
+            }
+            row[o_othm + q] = m;
+            ++q;
+        }
+        /* zone (:537-550) */
+        row[o_zone + 0] = e->zpos.x;
+        row[o_zone + 1] = e->zpos.y;
+        row[o_zone + 2] = e->zradius;
+        if (e->phase < e->cfg.zone_phases - 1) {
+            row[o_zone + 3] = e->zcent[e->phase + 1].x;
+            row[o_zone + 4] = e->zcent[e->phase + 1].y;
+            row[o_zone + 5] = (float)e->zrad[e->phase + 1];
+        }
+        /* the mask helpers zip(agents.bodies, cameras.seen) (:706-739) */
+        int p = post_pos[i];
+        int use_seen = e->alive[i] && p < e->cam_n;
+        if (H > 0) {
+            for (int h = 0; h < e->nheal && h < H; ++h) {
+                row[o_heal + 2 * h] = e->heal[h].pos.x;
+                row[o_heal + 2 * h + 1] = e->heal[h].pos.y;
+            }
+            for (int h = 0; h < H; ++h) {
+                float m;
+                if (e->cfg.omniscient) m = h < e->nheal ? 0.0f : 1.0f;
+                else m = (h < e->nheal && use_seen && seen_has(e, p, e->heal[h].serial)) ? 0.0f : 1.0f;
+                row[o_healm + h] = m;
+            }
+        }
+        if (B > 0) {
+            for (int b = 0; b < e->nbox && b < B; ++b) {
+                for (int v = 0; v < 4; ++v) {
+                    row[o_box + 11 * b + 2 * v] = e->box[b].shape.v[v].x;
+                    row[o_box + 11 * b + 2 * v + 1] = e->box[b].shape.v[v].y;
+                }
+                row[o_box + 11 * b + 8] = e->box[b].pos.x;
+                row[o_box + 11 * b + 9] = e->box[b].pos.y;
+                row[o_box + 11 * b + 10] = e->box[b].angle;
+            }
+            for (int b = 0; b < B; ++b) {
+                float m;
+                if (e->cfg.omniscient) m = b < e->nbox ? 0.0f : 1.0f;
+                else m = (b < e->nbox && use_seen && seen_has(e, p, e->box[b].serial)) ? 0.0f : 1.0f;
+                row[o_boxm + b] = m;
+            }
+            for (int b = 0; b < e->nbi && b < B; ++b) {
+                for (int v = 0; v < 4; ++v) {
+                    row[o_bi + 10 * b + 2 * v] = e->bi[b].shape.v[v].x;
+                    row[o_bi + 10 * b + 2 * v + 1] = e->bi[b].shape.v[v].y;
+                }
+                row[o_bi + 10 * b + 8] = e->bi[b].pos.x;
+                row[o_bi + 10 * b + 9] = e->bi[b].pos.y;
+            }
+            for (int b = 0; b < B; ++b) {
+                float m;
+                if (e->cfg.omniscient) m = b < e->nbi ? 0.0f : 1.0f;
+                else m = (b < e->nbi && use_seen && seen_has(e, p, e->bi[b].serial)) ? 0.0f : 1.0f;
+                row[o_bim + b] = m;
+            }
+        }
+        /* inventory slots (:620-654) */
+        if (H > 0) row[o_hsm] = 1.0f;
+        if (B > 0) row[o_bsm] = 1.0f;
+        if (e->alive[i] && e->inv_n[i] > 0) {
+            const item* it = &e->inv[i][e->inv_n[i] - 1];
+            if (H > 0 && it->kind == IT_HEAL) {
+                row[o_hs] = (float)e->cfg.healing;
+                row[o_hsm] = 0.0f;
+            }
+            if (B > 0 && it->kind == IT_BOX) {
+                for (int v = 0; v < 4; ++v) {
+                    row[o_bs + 2 * v] = it->shape.v[v].x;
+                    row[o_bs + 2 * v + 1] = it->shape.v[v].y;
+                }
+                row[o_bsm] = 0.0f;
+            }
+        }
+    }
+}
+
+/* SafeZone (semantics.py:739-811) */
+static void zone_set_phase_zone(ora_env* e)
+{
+    e->zradius = (float)e->zrad[e->phase];
+    e->zpos = e->zcent[e->phase];
+}
+
+static void zone_tick(ora_env* e)
+{
+    int shrinking = e->t_cooldown == 0;
+    if (shrinking) {
+        if (e->endgame) return;
+        e->t_shrink -= 1;
+        if (e->t_shrink > 0) {
+            double t = (double)e->t_shrink / (double)e->cfg.zone_cooldown;
+            double r1 = e->zrad[e->phase], r2 = e->zrad[e->phase + 1];
+            v2 c1 = e->zcent[e->phase], c2 = e->zcent[e->phase + 1];
+            double radius = t * r1 + (1.0 - t) * r2;
+            float tf = (float)t, tf1 = (float)(1.0 - t);
+            e->zradius = (float)radius;
+            e->zpos = vadd(smul(tf, c1), smul(tf1, c2));
+            return;
+        }
+        e->t_cooldown = e->cfg.zone_cooldown;
+        e->phase += 1;
+        zone_set_phase_zone(e);
+        if (e->phase == e->cfg.zone_phases - 1) e->endgame = 1;
+    } else {
+        e->t_cooldown -= 1;
+        if (e->t_cooldown > 0) return;
+        e->t_shrink = e->cfg.zone_cooldown;
+    }
+}
+
+void ora_env_reset(ora_env* e, float* obs)
+{
+    const mas_config* cfg = &e->cfg;
+    int A = e->A, H = e->H, B = e->B;
+    /* SpawnGrid.reset (semantics.py:71-74) */
+    int n = e->ngrid;
+    v2 pos[4096];
+    memcpy(pos, e->grid, sizeof(v2) * (size_t)n);
+    for (int i = n - 1; i >= 1; --i) {
+        int j = (int)ora_random_interval(&e->rng, (uint64_t)i);
+        v2 t = pos[i]; pos[i] = pos[j]; pos[j] = t;
+    }
+    int top = n;
+    /* Simulation.reset: new world (simulation.py:228-231) */
+    memset(&e->w.aa, 0, sizeof(e->w.aa));
+    memset(&e->w.as, 0, sizeof(e->w.as));
+    e->w.inv_dt0 = 0.0f;
+    e->next_serial = 1;
+    /* boxes: RandomizeBoxShapes, ResetSpawns, Object, IndexBodies, Health */
+    poly shapes[OB];
+    for (int b = 0; b < B; ++b) {
+        if (cfg->randomized_boxes) {
+            /* Python max(rng.normal(loc, scale), min): loc + scale * gauss */
+            double wv = cfg->avg_w + cfg->std_w * ora_standard_normal(&e->rng);
+            wv = cfg->min_w > wv ? cfg->min_w : wv;
+            double hv = cfg->avg_h + cfg->std_h * ora_standard_normal(&e->rng);
+            hv = cfg->min_h > hv ? cfg->min_h : hv;
+            ora_poly_set_as_box(&shapes[b], (float)(wv / 2.0), (float)(hv / 2.0));
+        } else {
+            ora_poly_set_as_box(&shapes[b], (float)(cfg->box_size / 2.0), (float)(cfg->box_size / 2.0));
+        }
+    }
+    e->nbox = 0;
+    for (int b = 0; b < B; ++b) {
+        box_t* bx = &e->box[e->nbox++];
+        bx->serial = e->next_serial++;
+        bx->pos = pos[--top];
+        bx->angle = 0.0f;
+        bx->q = rot_of(0.0f);
+        bx->shape = shapes[b];
+        bx->health = cfg->box_health;
+        bx->hinit = 1;
+        bx->vuln = CAUSE_NONE;
+        bx->cause = CAUSE_NONE;
+    }
+    e->npend = 0;
+    e->nbi = 0;
+    /* heals */
+    e->nheal = 0;
+    for (int h = 0; h < H; ++h) spawn_heal(e, pos[--top]);
+    /* walls */
+    for (int k = 0; k < NWALLS; ++k) e->wall_serial[k] = e->next_serial++;
+    /* agents */
+    for (int i = 0; i < A; ++i) {
+        e->aserial[i] = e->next_serial++;
+        e->w.active[i] = 1;
+        e->w.c[i] = pos[--top];
+        e->w.a[i] = 0.0f;
+        e->w.v[i] = V(0.0f, 0.0f);
+        e->w.w[i] = 0.0f;
+        e->w.sleep_time[i] = 0.0f;
+        e->w.awake[i] = 1;
+        e->alive[i] = 1;
+        e->health[i] = cfg->agent_health;
+        e->cause[i] = CAUSE_NONE;
+        e->cooldown[i] = 0;
+        e->inv_n[i] = 0;
+    }
+    sync_statics(e);
+    update_seen(e);
+    /* SafeZone.post_reset */
+    int nr = cfg->zone_n_radii;
+    for (int k = 0; k < nr; ++k) e->zrad[k] = cfg->zone_radii[k];
+    e->zrad[nr] = 0.0;
+    if (cfg->zone_random_centers) {
+        v2 rev[MAS_MAX_ZONE_PHASES + 1];
+        for (int k = nr, q = 0; k >= 0; --k, ++q) {
+            double L = cfg->floor_size - 2.0 * e->zrad[k];
+            double cx = (ora_pcg64_random(&e->rng) * L) - L / 2.0;
+            double cy = (ora_pcg64_random(&e->rng) * L) - L / 2.0;
+            rev[q] = V((float)cx, (float)cy);
+        }
+        for (int k = 0; k <= nr; ++k) e->zcent[k] = rev[nr - k];
+    } else {
+        for (int k = 0; k < nr; ++k) e->zcent[k] = V(cfg->zone_centers[k][0], cfg->zone_centers[k][1]);
+        e->zcent[nr] = V(0.0f, 0.0f);
+    }
+    e->t_cooldown = cfg->zone_cooldown;
+    e->t_shrink = 0;
+    e->phase = 0;
+    e->endgame = 0;
+    zone_set_phase_zone(e);
+    e->ndeaths = 0;
+    e->nkills = 0;
+    e->uses_heal = 0;
+    e->uses_box = 0;
+    e->steps = 0;
+    if (obs) write_obs(e, obs);
+}
+
+/* Inventory.take (semantics.py:179-187) for one item */
+static int inv_take(ora_env* e, int i, const item* it)
+{
+    if (1 + e->inv_n[i] > e->cfg.slots) return 0;
+    e->inv[i][e->inv_n[i]++] = *it;
+    return 1;
+}
+
+int32_t ora_env_step(ora_env* e, const int8_t* actions, float* obs, float* rewards)
+{
+    const mas_config* cfg = &e->cfg;
+    int A = e->A;
+    static const float dmap[3] = {-1.0f, 0.0f, 1.0f};
+    /* queue_actions (masurvival_env.py:741-755) */
+    int ctl[OA][6];
+    for (int i = 0; i < A; ++i) {
+        for (int k = 0; k < 6; ++k) ctl[i][k] = actions[i * 6 + k];
+    }
+    /* ---------------- pre_step ---------------- */
+    /* boxes: Object.pre_step (semantics.py:853-856) */
+    for (int k = 0; k < e->npend; ++k) spawn_bitem(e, e->pend[k].pos, &e->pend[k].shape, e->pend[k].owner);
+    e->npend = 0;
+    /* agents: DynamicMotors (simulation.py:407-424) */
+    for (int i = 0; i < A; ++i) {
+        if (!e->alive[i]) continue;
+        rot q = rot_of(e->w.a[i]);
+        float par = dmap[ctl[i][0]] * cfg->impulse[0];
+        float nor = dmap[ctl[i][1]] * cfg->impulse[1];
+        v2 J = V(q.c * par + (-q.s) * nor, q.s * par + q.c * nor);
+        float ang = dmap[ctl[i][2]] * cfg->impulse[2];
+        wake(&e->w, i);
+        e->w.v[i] = vadd(e->w.v[i], smul(e->w.inv_mass, J));
+        e->w.w[i] += e->w.inv_I * crossvv(vsub(e->w.c[i], e->w.c[i]), J);
+        e->w.w[i] += e->w.inv_I * ang;
+    }
+    /* UseLast (semantics.py:300-309) */
+    for (int i = 0; i < A; ++i) {
+        if (!e->alive[i] || !ctl[i][4] || e->inv_n[i] == 0) continue;
+        item it = e->inv[i][--e->inv_n[i]];
+        if (it.kind == IT_HEAL) {
+            e->uses_heal++;
+            g_cnt[CNT_HEAL_USED]++;
+            agent_change_health(e, i, cfg->healing, CAUSE_NONE); /* Heal.use :646-649 */
+        } else if (it.kind == IT_BOX) {
+            e->uses_box++;
+            g_cnt[CNT_BOX_PLACED]++;
+            v2 off = from_polar(cfg->box_item_offset, e->w.a[i]); /* ObjectItem.use :830-836 */
+            spawn_box(e, vadd(e->w.c[i], off), &it.shape, cfg->ownership ? it.owner : CAUSE_NONE);
+        }
+    }
+    /* GiveLast (semantics.py:335-370) */
+    {
+        bref bodies[4 * OB + OH + OA + NWALLS];
+        int nb = all_bodies(e, bodies);
+        bref taker[OA];
+        for (int i = 0; i < A; ++i) {
+            taker[i].kind = -1;
+            if (!e->alive[i]) continue;
+            float mind = INFINITY;
+            for (int k = 0; k < nb; ++k) {
+                v2 oc = body_pos(e, bodies[k]);
+                if (!ora_circle_test_point(cfg->give_radius, e->w.c[i], oc)) continue;
+                if (bodies[k].kind == K_AGENT && bodies[k].idx == i) continue;
+                float dist = vlen(vsub(e->w.c[i], oc));
+                if (dist < mind) { mind = dist; taker[i] = bodies[k]; }
+            }
+        }
+        for (int i = 0; i < A; ++i) {
+            if (!e->alive[i] || !ctl[i][5] || taker[i].kind < 0) continue;
+            if (taker[i].kind != K_AGENT) continue; /* no Inventory in the taker's group */
+            int t = taker[i].idx;
+            if (cfg->teams && team_of(e, t) != team_of(e, i)) continue; /* strangers */
+            if (e->inv_n[i] == 0) continue;
+            item it = e->inv[i][--e->inv_n[i]];
+            if (inv_take(e, t, &it)) g_cnt[CNT_GIVE_OK]++;
+            else g_cnt[CNT_GIVE_LOST]++; /* full: the item is lost (quirk D3) */
+        }
+    }
+    /* Melee / ContinuousMelee (semantics.py:531-554, 584-610) */
+    {
+        bref target[OA];
+        for (int i = 0; i < A; ++i) {
+            target[i].kind = -1;
+            if (!e->alive[i]) continue;
+            v2 hand = from_polar(cfg->melee_range, e->w.a[i]);
+            v2 endp = vadd(e->w.c[i], hand);
+            target[i] = ray_cast(e, e->w.c[i], endp);
+        }
+        for (int i = 0; i < A; ++i) {
+            if (!e->alive[i]) continue;
+            int on_cd = e->melee_cd > 0 && e->cooldown[i] > 0;
+            if (target[i].kind >= 0 && ctl[i][3] && !on_cd) {
+                int cause = cfg->teams ? CAUSE_BADGE0 + team_of(e, i) : i;
+                if (target[i].kind == K_AGENT) agent_change_health(e, target[i].idx, -cfg->melee_damage, cause);
+                else if (target[i].kind == K_BOX) box_change_health(e, target[i].idx, -cfg->melee_damage, cause);
+                if (e->melee_cd > 0) e->cooldown[i] = e->melee_cd;
+            }
+        }
+        if (e->melee_cd > 0) {
+            for (int i = 0; i < A; ++i)
+                if (e->cooldown[i] > 0) e->cooldown[i] -= 1;
+        }
+    }
+    /* ---------------- physics: 2 x world.Step(1/60, 10, 10) ---------------- */
+    for (int i = 0; i < A; ++i) e->w.active[i] = e->alive[i];
+    for (int s = 0; s < 2; ++s) ora_world_step(&e->w, (float)(1.0 / 60.0), 10, 10);
+    /* ---------------- post_step ---------------- */
+    /* boxes: Health.post_step (semantics.py:429-435) + Object/OwnedObject despawn */
+    for (int b = 0; b < e->nbox; ++b) {
+        if (!e->box[b].hinit) { e->box[b].hinit = 1; e->box[b].health = cfg->box_health; }
+    }
+    for (int b = 0; b < e->nbox;) {
+        if (e->box[b].health <= 0) {
+            pend_t* p = &e->pend[e->npend++];
+            p->pos = e->box[b].pos;
+            ora_poly_set(&p->shape, e->box[b].shape.v, e->box[b].shape.count); /* prototype() copy_shape */
+            p->owner = e->box[b].cause;
+            g_cnt[CNT_BOX_BROKEN]++;
+            despawn_box(e, b);
+        } else {
+            ++b;
+        }
+    }
+    /* agents: Cameras.post_step (pre-despawn list) */
+    update_seen(e);
+    /* agents: Health.post_step -> despawn dead (id order) */
+    {
+        int dead[OA], nd = 0;
+        for (int i = 0; i < A; ++i)
+            if (e->alive[i] && e->health[i] <= 0) dead[nd++] = i;
+        if (nd > 0) {
+            for (int q = 0; q < nd; ++q) e->deaths[e->ndeaths++] = dead[q]; /* TrackDeaths */
+            /* DeathDrop (semantics.py:387-396) */
+            int total = 0;
+            for (int q = 0; q < nd; ++q) total += e->inv_n[dead[q]];
+            double angles[OA * ORA_MAX_SLOTS];
+            for (int k = 0; k < total; ++k) angles[k] = 2.0 * M_PI * ora_pcg64_random(&e->rng);
+            g_cnt[CNT_DROP_ITEMS] += total;
+            int top = total;
+            for (int q = 0; q < nd; ++q) {
+                int i = dead[q];
+                int full = e->inv_n[i];
+                float ang[ORA_MAX_SLOTS];
+                for (int k = 0; k < full; ++k) ang[k] = (float)angles[--top];
+                for (int k = 0; k < full; ++k) {
+                    v2 off = from_polar(cfg->deathdrop_radius, ang[k]);
+                    v2 p = vadd(e->w.c[i], off);
+                    if (e->inv[i][k].kind == IT_HEAL) spawn_heal(e, p);
+                    else spawn_bitem(e, p, &e->inv[i][k].shape, e->inv[i][k].owner);
+                }
+                e->inv_n[i] = 0;
+            }
+            for (int q = 0; q < nd; ++q) {
+                int i = dead[q];
+                e->kills_cause[e->nkills++] = e->cause[i]; /* TrackKills via on_death */
+                e->alive[i] = 0;
+                e->w.active[i] = 0;
+                for (int j = 0; j < A; ++j) {
+                    memset(&e->w.aa[i][j], 0, sizeof(ora_cmem));
+                    memset(&e->w.aa[j][i], 0, sizeof(ora_cmem));
+                }
+                for (int s = 0; s < ORA_MAX_STAT; ++s) memset(&e->w.as[i][s], 0, sizeof(ora_cmem));
+            }
+        }
+    }
+    /* AutoPickup.post_step (semantics.py:278-283) */
+    {
+        bref bodies[4 * OB + OH + OA + NWALLS];
+        int nb = all_bodies(e, bodies);
+        /* per agent: items in range, snapshot (serial, kind, data) */
+        typedef struct { uint32_t serial; int kind; item it; } cand;
+        static __thread cand lists[OA][OB + OH];
+        int nl[OA];
+        for (int i = 0; i < A; ++i) {
+            nl[i] = 0;
+            if (!e->alive[i]) continue;
+            for (int k = 0; k < nb; ++k) {
+                if (bodies[k].kind != K_HEAL && bodies[k].kind != K_BITEM) continue;
+                v2 oc = body_pos(e, bodies[k]);
+                if (!ora_circle_test_point(cfg->pickup_radius, e->w.c[i], oc)) continue;
+                cand* c = &lists[i][nl[i]++];
+                c->serial = body_serial(e, bodies[k]);
+                c->kind = bodies[k].kind;
+                if (c->kind == K_HEAL) {
+                    c->it.kind = IT_HEAL;
+                    c->it.owner = CAUSE_NONE;
+                    memset(&c->it.shape, 0, sizeof(poly));
+                } else {
+                    c->it.kind = IT_BOX;
+                    c->it.shape = e->bi[bodies[k].idx].shape;
+                    c->it.owner = e->bi[bodies[k].idx].owner;
+                }
+            }
+        }
+        for (int i = 0; i < A; ++i) {
+            for (int k = 0; k < nl[i]; ++k) {
+                if (!inv_take(e, i, &lists[i][k].it)) continue;
+                g_cnt[CNT_ITEM_PICKED]++;
+                int found = 0;
+                /* despawn the item if it is still in its group (quirk D4) */
+                if (lists[i][k].kind == K_HEAL) {
+                    for (int h = 0; h < e->nheal; ++h) {
+                        if (e->heal[h].serial == lists[i][k].serial) {
+                            found = 1;
+                            for (int q = h; q + 1 < e->nheal; ++q) e->heal[q] = e->heal[q + 1];
+                            e->nheal--;
+                            break;
+                        }
+                    }
+                } else {
+                    for (int b = 0; b < e->nbi; ++b) {
+                        if (e->bi[b].serial == lists[i][k].serial) {
+                            found = 1;
+                            for (int q = b; q + 1 < e->nbi; ++q) e->bi[q] = e->bi[q + 1];
+                            e->nbi--;
+                            break;
+                        }
+                    }
+                }
+                if (!found) g_cnt[CNT_DOUBLE_PICK]++;
+            }
+        }
+    }
+    /* SafeZone.post_step (semantics.py:758-768) */
+    for (int i = 0; i < A; ++i) {
+        if (!e->alive[i]) continue;
+        if (e->endgame || !ora_circle_test_point(e->zradius, e->zpos, e->w.c[i]))
+            agent_change_health(e, i, -cfg->zone_damage, CAUSE_ZONE);
+    }
+    zone_tick(e);
+    /* ---------------- observations / rewards / done ---------------- */
+    if (obs) write_obs(e, obs);
+    /* compute_rewards (masurvival_env.py:757-803) */
+    float rew[OA];
+    for (int i = 0; i < A; ++i) rew[i] = 0.0f;
+    if (!cfg->teams) {
+        for (int i = 0; i < A; ++i) e->last_kills[i] = 0;
+        for (int i = 0; i < A; ++i) rew[i] += e->alive[i] ? cfg->r_alive : cfg->r_dead;
+        int any_dead = 0, first_dead = -1;
+        for (int i = 0; i < A; ++i)
+            if (!e->alive[i]) { any_dead = 1; if (first_dead < 0) first_dead = i; }
+        for (int k = 0; k < e->nkills; ++k) {
+            int c = e->kills_cause[k];
+            int idx = -1;
+            if (c >= 0 && c < A && e->alive[c]) idx = c;
+            else if (c == CAUSE_NONE && any_dead) idx = first_dead; /* None in indexed_agents */
+            if (idx >= 0) {
+                rew[idx] += cfg->r_kill;
+                e->last_kills[idx] += 1;
+            }
+        }
+        for (int k = 0; k < e->ndeaths; ++k) rew[e->deaths[k]] += cfg->r_death;
+    } else {
+        e->last_kills[0] = e->last_kills[1] = 0;
+        for (int t = 0; t < 2; ++t) {
+            int alive_t = 0;
+            for (int i = 0; i < A; ++i)
+                if (team_of(e, i) == t && e->alive[i]) alive_t = 1;
+            for (int i = 0; i < A; ++i)
+                if (team_of(e, i) == t) rew[i] += alive_t ? cfg->r_alive : cfg->r_dead;
+        }
+        for (int k = 0; k < e->nkills; ++k) {
+            int c = e->kills_cause[k];
+            if (c != CAUSE_BADGE0 && c != CAUSE_BADGE0 + 1) continue;
+            int t = c - CAUSE_BADGE0;
+            for (int i = 0; i < A; ++i)
+                if (team_of(e, i) == t) rew[i] += cfg->r_kill;
+            e->last_kills[t] += 1;
+        }
+        for (int k = 0; k < e->ndeaths; ++k) {
+            int t = team_of(e, e->deaths[k]);
+            for (int i = 0; i < A; ++i)
+                if (team_of(e, i) == t) rew[i] += cfg->r_death;
+        }
+    }
+    e->nkills = 0;
+    e->ndeaths = 0;
+    for (int i = 0; i < A; ++i) e->last_rewards[i] = rew[i];
+    if (rewards) memcpy(rewards, rew, sizeof(float) * (size_t)A);
+    /* is_done (masurvival_env.py:810-831) */
+    int n_alive = 0;
+    if (cfg->teams) {
+        for (int t = 0; t < 2; ++t) {
+            int at = 0;
+            for (int i = 0; i < A; ++i)
+                if (team_of(e, i) == t && e->alive[i]) at = 1;
+            n_alive += at;
+        }
+    } else {
+        for (int i = 0; i < A; ++i) n_alive += e->alive[i];
+    }
+    int done = cfg->gameover_mode == 1 ? (n_alive <= 1) : (n_alive == 0);
+    e->steps += 1;
+    /* _update_stats (masurvival_env.py:483-508) */
+    {
+        int R = cfg->teams ? 2 : A;
+        if (!e->stats_init) { memset(e->stats, 0, sizeof(e->stats)); e->stats_init = 1; }
+        for (int r = 0; r < R; ++r) {
+            int j = cfg->teams ? (r == 0 ? 0 : A / 2) : r;
+            e->stats[r] += e->last_rewards[j];
+            e->stats[8 + r] += (float)e->last_kills[r];
+        }
+        e->stats[16] += 1.0f;
+        e->stats[17] += (float)e->uses_heal;
+        e->stats[18] += (float)e->uses_box;
+        e->uses_heal = 0;
+        e->uses_box = 0;
+    }
+    return done;
+}
+
+void ora_env_flush_stats(ora_env* e, float* stats)
+{
+    if (!e->stats_init) { memset(e->stats, 0, sizeof(e->stats)); e->stats_init = 1; }
+    memcpy(stats, e->stats, sizeof(e->stats));
+    memset(e->stats, 0, sizeof(e->stats));
+}
+
+int32_t ora_env_debug(const ora_env* e, float* out, int32_t cap)
+{
+    int n = 0;
+#define PUT(x) do { if (n < cap) out[n] = (float)(x); ++n; } while (0)
+    for (int i = 0; i < e->A; ++i) {
+        PUT(e->alive[i]); PUT(e->health[i]); PUT(e->w.c[i].x); PUT(e->w.c[i].y); PUT(e->w.a[i]);
+        PUT(e->w.v[i].x); PUT(e->w.v[i].y); PUT(e->w.w[i]); PUT(e->w.awake[i]); PUT(e->w.sleep_time[i]);
+        PUT(e->cooldown[i]); PUT(e->inv_n[i]); PUT(e->cause[i]);
+    }
+    PUT(e->nbox); PUT(e->nbi); PUT(e->nheal); PUT(e->npend);
+    PUT(e->phase); PUT(e->t_cooldown); PUT(e->t_shrink); PUT(e->endgame);
+#undef PUT
+    return n;
+}

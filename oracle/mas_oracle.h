@@ -1,0 +1,95 @@
+/*
+ * mas_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Scalar CPU restatement of the reference env step (KRLGroup/gym-ma-survival-2d
+ * masurvival/{simulation,semantics}.py + envs/masurvival_env.py) together with
+ * the subset of Box2D 2.3.x that PyBox2D 2.3.10 executes for it.  It is the
+ * parity checker for the HIP path and the CPU baseline of bench.py; nothing in
+ * the product (gym-ma-survival-2d_amd/) links, loads or calls it.
+ */
+#ifndef MAS_ORACLE_H
+#define MAS_ORACLE_H
+
+#include <stdint.h>
+#include "../include/masurvival.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORA_MAX_DYN 16
+#define ORA_MAX_STAT 72
+#define ORA_MAX_SLOTS 16
+
+typedef struct { float x, y; } ora_v2;
+typedef struct { float s, c; } ora_rot;
+typedef struct { int32_t count; ora_v2 v[8]; ora_v2 n[8]; } ora_poly;
+typedef struct { int32_t touching; float ni, ti; } ora_cmem;
+
+/* A Box2D world reduced to what MaSurvival puts in it: dynamic circles
+ * (agents, canonical order = agent id) and static polygons (canonical order =
+ * walls in ThickRoomWalls order, then boxes in group list order).  Sensors
+ * (heals, box items) never enter the solver and are not represented. */
+typedef struct ora_world {
+    int32_t n_dyn;
+    int32_t active[ORA_MAX_DYN];
+    ora_v2 c[ORA_MAX_DYN];
+    float a[ORA_MAX_DYN];
+    ora_v2 v[ORA_MAX_DYN];
+    float w[ORA_MAX_DYN];
+    float sleep_time[ORA_MAX_DYN];
+    int32_t awake[ORA_MAX_DYN];
+    float radius, inv_mass, inv_I, lin_damp, ang_damp;
+    int32_t n_stat;
+    ora_v2 sp[ORA_MAX_STAT];
+    float sa[ORA_MAX_STAT];
+    ora_rot sq[ORA_MAX_STAT];
+    ora_poly spoly[ORA_MAX_STAT];
+    ora_cmem aa[ORA_MAX_DYN][ORA_MAX_DYN];
+    ora_cmem as[ORA_MAX_DYN][ORA_MAX_STAT];
+    float inv_dt0;
+} ora_world;
+
+/* -------- primitives (exported for the test-only Box2D shim) -------- */
+void ora_sincos(float angle, float* s, float* c);
+void ora_poly_set_as_box(ora_poly* p, float hx, float hy);
+void ora_poly_set(ora_poly* p, const ora_v2* verts, int32_t count);
+int32_t ora_poly_test_point(const ora_poly* p, ora_v2 xp, ora_rot xq, ora_v2 pt);
+int32_t ora_circle_test_point(float radius, ora_v2 center, ora_v2 pt);
+int32_t ora_ray_circle(float radius, ora_v2 center, ora_v2 p1, ora_v2 p2, float max_fraction, float* fraction);
+int32_t ora_ray_poly(const ora_poly* p, ora_v2 xp, ora_rot xq, ora_v2 p1, ora_v2 p2, float max_fraction, float* fraction);
+void ora_body_mass(float radius, float density, float* inv_mass, float* inv_I);
+void ora_world_step(ora_world* w, float dt, int32_t vel_iters, int32_t pos_iters);
+int32_t ora_world_sizeof(void);
+
+/* -------- numpy Generator(PCG64) restatement -------- */
+typedef struct { uint64_t st_hi, st_lo, inc_hi, inc_lo; int32_t has_uint32; uint32_t uinteger; } ora_pcg64;
+uint64_t ora_pcg64_next64(ora_pcg64* r);
+uint32_t ora_pcg64_next32(ora_pcg64* r);
+double ora_pcg64_random(ora_pcg64* r);
+uint64_t ora_random_interval(ora_pcg64* r, uint64_t max);
+double ora_standard_normal(ora_pcg64* r);
+
+/* -------- env -------- */
+typedef struct ora_env ora_env;
+ora_env* ora_env_create(const mas_config* cfg, char* err, int32_t errlen);
+void ora_env_destroy(ora_env* e);
+int32_t ora_env_obs_dim(const ora_env* e);
+void ora_env_set_rng(ora_env* e, const uint64_t* st6);
+void ora_env_get_rng(const ora_env* e, uint64_t* st6);
+void ora_env_reset(ora_env* e, float* obs);
+/* returns done */
+int32_t ora_env_step(ora_env* e, const int8_t* actions, float* obs, float* rewards);
+void ora_env_flush_stats(ora_env* e, float* stats /* MAS_STATS_WIDTH */);
+/* coverage counters: TOI events, TOI restores, sleeps, boxes broken/placed,
+ * items picked, gives ok/lost, dropped items, heals used, double pickups,
+ * agent-agent solver contacts */
+#define ORA_NCOUNTERS 12
+void ora_counters(int64_t* out, int32_t reset);
+/* compact state digest for debugging (agent kinematics + health + inventory sizes) */
+int32_t ora_env_debug(const ora_env* e, float* out, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
