@@ -1,0 +1,150 @@
+"""Headline benchmark: agent-env-steps/sec for the 2v2 config.
+
+A "step" is one batched MaSurvival.step of every env on this rank (the HIP
+k_step kernel: actions -> 2 Box2D steps -> rules -> obs/rewards/done, with
+auto-reset), inputs resident in HBM.  Actions come from a device RNG
+(random policy) drawn before the timed kernel on the same stream.
+
+Run: python bench.py [--gpus N --steps K --warmup W --config 2v2 --envs N_per_gpu]
+For N>1 the driver launches one rank per GPU with torch.distributed.run; envs
+shard with no data-path collective (weak scaling).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'gym-ma-survival-2d_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def algorithmic_bytes_per_env_step(A, H, B, D):
+    """Bstep = 8*S + 6A + 4*A*D + 4A + 1 with
+    S = 27A + 14B + 3H + 17 + 2*(A(A-1)/2 + A(B+4)) + 4 persistent words."""
+    S = 27 * A + 14 * B + 3 * H + 17 + 2 * (A * (A - 1) // 2 + A * (B + 4)) + 4
+    return 8 * S + 6 * A + 4 * A * D + 4 * A + 1
+
+
+def cpu_baseline(cfg, budget_s=12.0):
+    """The C oracle (scalar restatement, 1 thread) on a bounded sample: round-robin
+    over 64 envs of the same config with uniform random actions, until budget_s."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    from oracle import OracleEnv
+    from masurvival.config import ResolvedConfig, pcg64_state
+    rc = ResolvedConfig(cfg)
+    n = 64
+    envs = [OracleEnv(rc.to_struct(), pcg64_state(s)) for s in range(n)]
+    for e in envs:
+        e.reset()
+    rng = np.random.default_rng(1)
+    acts = rng.integers(0, [3, 3, 3, 2, 2, 2], size=(256, n, rc.n_agents, 6)).astype(np.int8)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        a = acts[(steps // n) % 256]
+        for i, e in enumerate(envs):
+            _, _, d = e.step(a[i])
+            if d:
+                e.reset()
+        steps += n
+    dt = time.perf_counter() - t0
+    return {'value': steps * rc.n_agents / dt, 'unit': 'agent-env-steps/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{steps} env-steps ({n} envs round-robin, random actions, auto-reset) of the C oracle, '
+                      f'1 thread, {dt:.1f}s incl. ctypes per-step call overhead'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--config', default='2v2')
+    ap.add_argument('--envs', type=int, default=None, help='envs per GPU (default 65536 for 2v2)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    from masurvival.config import NAMED_CONFIGS
+    from masurvival.vec_env import VecMaSurvival
+    cfg = NAMED_CONFIGS[args.config]
+    n = args.envs or {'1v1': 4096, '2v2': 65536, 'ffa4': 16384}[args.config]
+    env = VecMaSurvival(cfg, n_envs=n, seeds=range(rank * n, rank * n + n), auto_reset=True)
+    A, D = env.n_agents, env.obs_dim
+    dev = env.device
+    env.reset()
+    hi = torch.tensor([3, 3, 3, 2, 2, 2], device=dev, dtype=torch.int32)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    acts = torch.empty((n, A, 6), dtype=torch.int8, device=dev)
+
+    def draw():
+        u = torch.rand((n, A, 6), generator=gen, device=dev)
+        acts.copy_((u * hi).to(torch.int8))
+
+    for _ in range(args.warmup):
+        draw()
+        env.step(acts)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        draw()
+        ev[k][0].record()
+        env.step(acts)
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, kern_ms = float(t[0]), float(t[1])
+
+    total_agent_steps = world * n * A * args.steps
+    b_env = algorithmic_bytes_per_env_step(A, env.rc.n_heals, env.rc.n_boxes, D)
+    achieved = b_env * n / (kern_ms * 1e-3) / 1e9
+    line = {
+        'metric': 'agent-env-steps/sec (whole node), %s N_envs=%d' % (args.config, n * world),
+        'value': total_agent_steps / dt,
+        'unit': 'agent-env-steps/s',
+        'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': dt * 1e3 / args.steps,
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'f32', 'data': 'synthetic (device-RNG random policy)',
+        'config': {'workload': f'{args.config} env step, N_envs={n}/GPU, auto-reset, random policy',
+                   'n_envs_per_gpu': n, 'n_agents': A, 'obs_dim': D, 'parallelism': f'env-shard x{world}'},
+        'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                     'kernel': 'k_step', 'kernel_ms': kern_ms, 'bytes_per_env_step': b_env},
+        'cpu_baseline': None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline(cfg)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

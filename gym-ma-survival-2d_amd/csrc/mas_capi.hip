@@ -1,0 +1,430 @@
+// mas_capi.hip -- host side of the C-ABI declared in include/masurvival.h:
+// config validation, capacity-class dispatch, Params (walls, vision cone, body
+// masses, observation layout) computed once per handle, HBM state
+// allocation, and the small seed / stats kernels.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/masurvival.h"
+#include "mas_env.h"
+
+#ifndef MAS_CLASS_LIST
+#define MAS_CLASS_LIST "?"
+#endif
+
+using namespace mas;
+
+namespace mas {
+struct ClassInfo {
+    int words, w_rng, w_has32, w_stats, lds_bytes;
+};
+#define MAS_DECLARE(NAME)                                                                                     \
+    ClassInfo class_info_##NAME();                                                                          \
+    void launch_step_##NAME(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const int8_t*, float*, float*, \
+                            uint8_t*, int);                                                                 \
+    void launch_reset_##NAME(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const uint8_t*, float*);
+#ifdef MAS_HAVE_1v1
+MAS_DECLARE(1v1)
+#endif
+#ifdef MAS_HAVE_2v2
+MAS_DECLARE(2v2)
+#endif
+#ifdef MAS_HAVE_ffa
+MAS_DECLARE(ffa)
+#endif
+#ifdef MAS_HAVE_xl
+MAS_DECLARE(xl)
+#endif
+}  // namespace mas
+
+namespace {
+
+constexpr int kWG = 64;  // threads per workgroup of k_step / k_reset (mas_step.h)
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(x)                                                                                       \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) return fail(MAS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+__global__ void k_seed(uint32_t* __restrict__ state, int64_t N, const uint64_t* __restrict__ st6, int w_rng,
+                       int w_has32)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    // st_hi, st_lo, inc_hi, inc_lo as (lo, hi) word pairs, then has32, u32
+    for (int k = 0; k < 4; ++k) {
+        uint64_t x = st6[e * 6 + k];
+        state[(int64_t)(w_rng + 2 * k) * N + e] = (uint32_t)(x & 0xffffffffULL);
+        state[(int64_t)(w_rng + 2 * k + 1) * N + e] = (uint32_t)(x >> 32);
+    }
+    state[(int64_t)w_has32 * N + e] = (uint32_t)st6[e * 6 + 4];
+    state[(int64_t)(w_has32 + 1) * N + e] = (uint32_t)st6[e * 6 + 5];
+}
+
+__global__ void k_stats(uint32_t* __restrict__ state, int64_t N, int w_stats, float* __restrict__ out)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    for (int k = 0; k < kStats; ++k) {
+        uint32_t u = state[(int64_t)(w_stats + k) * N + e];
+        float f;
+        __builtin_memcpy(&f, &u, 4);
+        out[e * kStats + k] = f;
+        state[(int64_t)(w_stats + k) * N + e] = 0u;
+    }
+}
+
+
+// generic Box2D b2PolygonShape::Set (weld, gift wrap, normals) for the cone
+Poly4 poly_set4(const V2* in)
+{
+    V2 ps[4];
+    int n = 0;
+    for (int i = 0; i < 4; ++i) {
+        bool uniq = true;
+        for (int j = 0; j < n; ++j)
+            if (dist2(in[i], ps[j]) < 0.5f * kLinearSlop) uniq = false;
+        if (uniq) ps[n++] = in[i];
+    }
+    int i0 = 0;
+    float x0 = ps[0].x;
+    for (int i = 1; i < n; ++i) {
+        float x = ps[i].x;
+        if (x > x0 || (x == x0 && ps[i].y < ps[i0].y)) {
+            i0 = i;
+            x0 = x;
+        }
+    }
+    int hull[8], m = 0, ih = i0;
+    for (;;) {
+        hull[m] = ih;
+        int ie = 0;
+        for (int j = 1; j < n; ++j) {
+            if (ie == ih) {
+                ie = j;
+                continue;
+            }
+            V2 r = sub(ps[ie], ps[hull[m]]);
+            V2 v = sub(ps[j], ps[hull[m]]);
+            float c = cross(r, v);
+            if (c < 0.0f) ie = j;
+            if (c == 0.0f && len2(v) > len2(r)) ie = j;
+        }
+        ++m;
+        ih = ie;
+        if (ie == i0 || m >= 8) break;
+    }
+    Poly4 P{};
+    for (int i = 0; i < 4 && i < m; ++i) P.v[i] = ps[hull[i]];
+    for (int i = 0; i < 4 && i < m; ++i) {
+        V2 e = sub(P.v[(i + 1) % m], P.v[i]);
+        P.n[i] = cross_vs(e, 1.0f);
+        normalize(P.n[i]);
+    }
+    return P;
+}
+
+}  // namespace
+
+struct Ops {
+    ClassInfo info;
+    void (*step)(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const int8_t*, float*, float*, uint8_t*, int);
+    void (*reset)(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const uint8_t*, float*);
+};
+
+struct mas_handle {
+    mas_config cfg;
+    Params P;
+    Ops ops;
+    int64_t N;
+    int device;
+    uint32_t* state;
+    uint64_t* seedbuf;
+    mas_obs_layout layout;
+};
+
+static void build_layout(mas_handle* h)
+{
+    const mas_config& c = h->cfg;
+    int A = c.n_agents, H = c.n_heals, B = c.n_boxes, as_ = 8 + (c.teams ? 1 : 0);
+    mas_obs_layout& L = h->layout;
+    memset(&L, 0, sizeof(L));
+    L.n_agents = A;
+    struct K { const char* name; int ndim, s0, s1; bool on; int* off; };
+    Params& P = h->P;
+    K keys[] = {
+        {"agent", 1, as_, 0, true, &P.o_agent},
+        {"box_items", 2, B, 10, B > 0, &P.o_bi},
+        {"box_items_mask", 1, B, 0, B > 0, &P.o_bim},
+        {"box_slot", 2, 1, 8, B > 0, &P.o_bs},
+        {"box_slot_mask", 1, 1, 0, B > 0, &P.o_bsm},
+        {"boxes", 2, B, 11, B > 0, &P.o_box},
+        {"boxes_mask", 1, B, 0, B > 0, &P.o_boxm},
+        {"heal_slot", 2, 1, 1, H > 0, &P.o_hs},
+        {"heal_slot_mask", 1, 1, 0, H > 0, &P.o_hsm},
+        {"heals", 2, H, 2, H > 0, &P.o_heal},
+        {"heals_mask", 1, H, 0, H > 0, &P.o_healm},
+        {"others", 2, A - 1, as_, true, &P.o_oth},
+        {"others_mask", 1, A - 1, 0, true, &P.o_othm},
+        {"zone", 1, 6, 0, true, &P.o_zone},
+    };
+    int off = 0, nk = 0;
+    for (auto& k : keys) {
+        *k.off = -1;
+        if (!k.on) continue;
+        *k.off = off;
+        snprintf(L.key_name[nk], 24, "%s", k.name);
+        L.key_offset[nk] = off;
+        L.key_ndim[nk] = k.ndim;
+        L.key_shape[nk][0] = k.s0;
+        L.key_shape[nk][1] = k.ndim > 1 ? k.s1 : 0;
+        off += k.s0 * (k.ndim > 1 ? k.s1 : 1);
+        ++nk;
+    }
+    L.n_keys = nk;
+    L.obs_dim = off;
+    P.D = off;
+}
+
+static int build_params(mas_handle* h)
+{
+    const mas_config& c = h->cfg;
+    Params& P = h->P;
+    memset(&P, 0, sizeof(P));
+    P.A = c.n_agents;
+    P.H = c.n_heals;
+    P.B = c.n_boxes;
+    P.slots = c.slots;
+    P.teams = c.teams;
+    P.ownership = c.ownership;
+    P.melee_cd = c.melee_cooldown;
+    P.omniscient = c.omniscient;
+    P.gameover = c.gameover_mode;
+    P.as_ = 8 + (c.teams ? 1 : 0);
+    P.r_alive = c.r_alive;
+    P.r_dead = c.r_dead;
+    P.r_kill = c.r_kill;
+    P.r_death = c.r_death;
+    P.imp0 = c.impulse[0];
+    P.imp1 = c.impulse[1];
+    P.imp2 = c.impulse[2];
+    P.agent_health = c.agent_health;
+    P.melee_range = c.melee_range;
+    P.melee_damage = c.melee_damage;
+    P.box_health = c.box_health;
+    P.box_hx = (float)(c.box_size / 2.0);
+    P.box_hy = (float)(c.box_size / 2.0);
+    P.randomized = c.randomized_boxes;
+    P.avg_w = c.avg_w;
+    P.std_w = c.std_w;
+    P.avg_h = c.avg_h;
+    P.std_h = c.std_h;
+    P.min_w = c.min_w;
+    P.min_h = c.min_h;
+    P.agent_r = (float)(c.agent_size / 2.0);
+    P.bitem_r = (float)(c.box_item_size / 2.0);
+    P.heal_r = (float)(c.heal_size / 2.0);
+    P.box_item_offset = c.box_item_offset;
+    P.healing = c.healing;
+    P.pickup_r = c.pickup_radius;
+    P.give_r = c.give_radius;
+    P.dd_r = c.deathdrop_radius;
+    P.zone_phases = c.zone_phases;
+    P.zone_cooldown = c.zone_cooldown;
+    P.zone_damage = c.zone_damage;
+    P.zone_nr = c.zone_n_radii;
+    P.zone_random = c.zone_random_centers;
+    for (int k = 0; k < kMaxPhases; ++k) {
+        P.zrad[k] = k < c.zone_n_radii ? c.zone_radii[k] : 0.0;
+        P.zradf[k] = (float)P.zrad[k];
+        if (k < MAS_MAX_ZONE_PHASES && k < c.zone_n_radii) {
+            P.zfix[k][0] = c.zone_centers[k][0];
+            P.zfix[k][1] = c.zone_centers[k][1];
+        }
+    }
+    P.floor_size = c.floor_size;
+    P.grid_size = c.grid_size;
+    // b2CircleShape::ComputeMass + b2Body::ResetMassData (density 1)
+    {
+        float r = P.agent_r;
+        float mass = 1.0f * kPi * r * r;
+        float I = mass * (0.5f * r * r + 0.0f);
+        float m = 0.0f + mass;
+        float bI = 0.0f + I;
+        P.inv_mass = 1.0f / m;
+        bI -= m * 0.0f;
+        P.inv_I = 1.0f / bI;
+    }
+    P.lin_damp = 0.8f;  // simulation.py:114 default_damping
+    P.ang_damp = 0.8f;
+    // ThickRoomWalls (semantics.py:685-695)
+    {
+        double height = c.floor_size, width = height / c.wall_aspect_ratio;
+        P.wall_poly = box_poly((float)(width / 2.0), (float)(height / 2.0), 0, 0);
+        double off = c.floor_size / 2.0;
+        P.wall_pos[0] = mk((float)(-off), 0.0f);
+        P.wall_pos[1] = mk(0.0f, (float)off);
+        P.wall_pos[2] = mk((float)off, 0.0f);
+        P.wall_pos[3] = mk(0.0f, (float)(-off));
+        P.wall_angle[0] = 0.0f;
+        P.wall_angle[1] = (float)(3.14159265358979323846 / 2.0);
+        P.wall_angle[2] = 0.0f;
+        P.wall_angle[3] = (float)(3.14159265358979323846 / 2.0);
+        for (int k = 0; k < kNumWalls; ++k) P.wall_q[k] = rot_of(P.wall_angle[k]);
+    }
+    // Cameras vision cone (simulation.py:321-328)
+    {
+        V2 left = from_polar(c.cam_depth, (float)(c.cam_fov / 2.0));
+        V2 center = mk(c.cam_depth, 0.0f);
+        V2 right = from_polar(c.cam_depth, (float)(-c.cam_fov / 2.0));
+        V2 vs[4] = {mk(0.0f, 0.0f), left, center, right};
+        P.cone = poly_set4(vs);
+    }
+    build_layout(h);
+    return MAS_OK;
+}
+
+extern "C" {
+
+const char* mas_last_error(void) { return g_err.c_str(); }
+int32_t mas_abi_version(void) { return MAS_ABI_VERSION; }
+
+int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle** out)
+{
+    if (!cfg || !out || n_envs <= 0) return fail(MAS_ERR_INVALID_ARG, "mas_create: null argument or n_envs <= 0");
+    const mas_config& c = *cfg;
+    if (c.n_agents < 2 || c.n_heals < 0 || c.n_boxes < 0 || c.slots < 0)
+        return fail(MAS_ERR_INVALID_ARG, "mas_create: n_agents must be >= 2 and counts non-negative");
+    if (c.grid_size * c.grid_size > 256 || c.n_agents + c.n_heals + c.n_boxes > c.grid_size * c.grid_size)
+        return fail(MAS_ERR_INVALID_ARG, "mas_create: spawn grid too large (>256 cells) or too small for the spawns");
+    if (c.zone_phases < 1 || c.zone_n_radii + 1 > kMaxPhases || c.zone_phases > c.zone_n_radii + 1)
+        return fail(MAS_ERR_INVALID_ARG, "mas_create: unsupported safe-zone phases");
+    mas_handle* h = new (std::nothrow) mas_handle();
+    if (!h) return fail(MAS_ERR_OOM, "mas_create: out of host memory");
+    h->cfg = c;
+    h->N = n_envs;
+    h->device = device;
+    auto fits = [&](int AM, int HM, int BM, int SM) {
+        return c.n_agents <= AM && c.n_heals <= HM && c.n_boxes <= BM && c.slots <= SM;
+    };
+    // capacity classes: (agents, heals, boxes, slots) -- see mas_k_<class>.hip
+    bool ok = false;
+#ifdef MAS_HAVE_1v1
+    if (!ok && fits(2, 4, 4, 4)) { h->ops = Ops{class_info_1v1(), launch_step_1v1, launch_reset_1v1}; ok = true; }
+#endif
+#ifdef MAS_HAVE_2v2
+    if (!ok && fits(4, 4, 4, 4)) { h->ops = Ops{class_info_2v2(), launch_step_2v2, launch_reset_2v2}; ok = true; }
+#endif
+#ifdef MAS_HAVE_ffa
+    if (!ok && fits(4, 16, 16, 4)) { h->ops = Ops{class_info_ffa(), launch_step_ffa, launch_reset_ffa}; ok = true; }
+#endif
+#ifdef MAS_HAVE_xl
+    if (!ok && fits(8, 16, 16, 8)) { h->ops = Ops{class_info_xl(), launch_step_xl, launch_reset_xl}; ok = true; }
+#endif
+    if (!ok) {
+        delete h;
+        return fail(MAS_ERR_UNSUPPORTED, "mas_create: no compiled capacity class fits this config (classes: " MAS_CLASS_LIST ")");
+    }
+    build_params(h);
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipMalloc(&h->state, (size_t)h->ops.info.words * (size_t)n_envs * 4);
+    if (e == hipSuccess) e = hipMemset(h->state, 0, (size_t)h->ops.info.words * (size_t)n_envs * 4);
+    if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
+    if (e != hipSuccess) {
+        std::string msg = std::string("mas_create: ") + hipGetErrorString(e);
+        if (h->state) hipFree(h->state);
+        delete h;
+        return fail(MAS_ERR_HIP, msg);
+    }
+    *out = h;
+    return MAS_OK;
+}
+
+int mas_destroy(mas_handle* h)
+{
+    if (!h) return MAS_OK;
+    if (h->state) hipFree(h->state);
+    if (h->seedbuf) hipFree(h->seedbuf);
+    delete h;
+    return MAS_OK;
+}
+
+int mas_get_obs_layout(const mas_handle* h, mas_obs_layout* out)
+{
+    if (!h || !out) return fail(MAS_ERR_INVALID_ARG, "mas_get_obs_layout: null argument");
+    *out = h->layout;
+    return MAS_OK;
+}
+
+int64_t mas_num_envs(const mas_handle* h) { return h ? h->N : -1; }
+
+int mas_seed(mas_handle* h, const uint64_t* host_rng_states, void* stream)
+{
+    if (!h || !host_rng_states) return fail(MAS_ERR_INVALID_ARG, "mas_seed: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(h->seedbuf, host_rng_states, (size_t)h->N * 6 * 8, hipMemcpyHostToDevice, s));
+    dim3 g((unsigned)((h->N + 255) / 256));
+    hipLaunchKernelGGL(k_seed, g, dim3(256), 0, s, h->state, h->N, h->seedbuf, h->ops.info.w_rng, h->ops.info.w_has32);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));  // host buffer may be released after return
+    return MAS_OK;
+}
+
+int mas_reset(mas_handle* h, const uint8_t* env_mask, float* obs, void* stream)
+{
+    if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_reset: null handle");
+    dim3 g((unsigned)((h->N + kWG - 1) / kWG));
+    h->ops.reset(g, (hipStream_t)stream, h->P, h->state, h->N, env_mask, obs);
+    HIP_TRY(hipGetLastError());
+    return MAS_OK;
+}
+
+int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, uint8_t* done, int32_t auto_reset,
+             void* stream)
+{
+    if (!h || !actions || !obs || !rewards || !done) return fail(MAS_ERR_INVALID_ARG, "mas_step: null argument");
+    dim3 g((unsigned)((h->N + kWG - 1) / kWG));
+    h->ops.step(g, (hipStream_t)stream, h->P, h->state, h->N, actions, obs, rewards, done, auto_reset);
+    HIP_TRY(hipGetLastError());
+    return MAS_OK;
+}
+
+int mas_flush_stats(mas_handle* h, float* stats, void* stream)
+{
+    if (!h || !stats) return fail(MAS_ERR_INVALID_ARG, "mas_flush_stats: null argument");
+    dim3 g((unsigned)((h->N + 255) / 256));
+    hipLaunchKernelGGL(k_stats, g, dim3(256), 0, (hipStream_t)stream, h->state, h->N, h->ops.info.w_stats, stats);
+    HIP_TRY(hipGetLastError());
+    return MAS_OK;
+}
+
+int64_t mas_state_bytes(const mas_handle* h) { return h ? (int64_t)h->ops.info.words * h->N * 4 : -1; }
+
+int mas_get_state(mas_handle* h, void* dst, void* stream)
+{
+    if (!h || !dst) return fail(MAS_ERR_INVALID_ARG, "mas_get_state: null argument");
+    HIP_TRY(hipMemcpyAsync(dst, h->state, (size_t)mas_state_bytes(h), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return MAS_OK;
+}
+
+int mas_set_state(mas_handle* h, const void* src, void* stream)
+{
+    if (!h || !src) return fail(MAS_ERR_INVALID_ARG, "mas_set_state: null argument");
+    HIP_TRY(hipMemcpyAsync(h->state, src, (size_t)mas_state_bytes(h), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return MAS_OK;
+}
+
+}  // extern "C"

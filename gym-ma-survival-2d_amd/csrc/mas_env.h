@@ -1,0 +1,394 @@
+// mas_env.h -- one MaSurvival env step per thread (gfx950 HIP).
+//
+// Layout: env state is struct-of-arrays in HBM (word w of env e at
+// state[w * N + e]): a wave loads / stores 64 consecutive envs' copies of a
+// field with one coalesced 256-B access.  Inside the kernel the env lives in
+// VGPRs (`EnvL`, every array statically indexed; runtime indices go through
+// the select helpers sel/put), so the whole step -- pre_step rules, two
+// Box2D-equivalent Steps, post_step rules, observation, reward, done and the
+// optional auto-reset -- runs without touching memory between the state
+// load and the state/obs store.
+//
+// Reference order is preserved exactly; every block
+// cites the reference lines it restates.  Canonical orders where Box2D's is
+// an implementation detail: queries/rays iterate groups in dict
+// order (boxes, box_items, heals, walls, agents), contacts are solved in
+// (agent-agent i<j, then agent-static agent-major) order.
+#pragma once
+
+#include "mas_math.h"
+#include "ziggurat_tables.h"
+
+namespace mas {
+
+// damage causes (Health.causes values, semantics.py:490-500)
+constexpr int kCauseNone = -1;
+constexpr int kCauseBadge = 64;  // + team id (TeamBadge, semantics.py:917-920)
+constexpr int kCauseZone = 96;   // SafeZone module instance
+
+constexpr int kItemNone = 0, kItemHeal = 1, kItemBox = 2;
+constexpr int kNumWalls = 4;
+constexpr int kMaxPhases = 9;   // zone radii incl. the appended 0
+constexpr int kStats = 19;      // MAS_STATS_WIDTH
+
+template <int AM_, int HM_, int BM_, int SM_, int KC_>
+struct Cap {
+    static constexpr int AM = AM_;  // agents
+    static constexpr int HM = HM_;  // heals
+    static constexpr int BM = BM_;  // boxes (= box items = pending drops)
+    static constexpr int SM = SM_;  // inventory slots
+    static constexpr int NS = kNumWalls + BM_;            // static bodies
+    static constexpr int NAA = AM_ * (AM_ - 1) / 2;       // agent-agent pairs
+    static constexpr int KC = KC_;                         // compact contact slots
+    static constexpr int NB = BM_ + BM_ + HM_ + kNumWalls + AM_;  // all bodies
+};
+
+// Per-config constants (host-computed, passed by value).
+struct Params {
+    int A, H, B, slots, teams, ownership, melee_cd, omniscient, gameover, D, as_;
+    float r_alive, r_dead, r_kill, r_death;
+    float imp0, imp1, imp2;
+    int agent_health;
+    float melee_range;
+    int melee_damage, box_health;
+    float box_hx, box_hy;
+    int randomized;
+    double avg_w, std_w, avg_h, std_h, min_w, min_h;
+    float agent_r, bitem_r, heal_r, box_item_offset;
+    int healing;
+    float pickup_r, give_r, dd_r;
+    int zone_phases, zone_cooldown, zone_damage, zone_nr, zone_random;
+    double zrad[kMaxPhases];
+    float zradf[kMaxPhases];
+    float zfix[kMaxPhases][2];
+    double floor_size;
+    int grid_size;
+    float inv_mass, inv_I, lin_damp, ang_damp;
+    Poly4 wall_poly;
+    V2 wall_pos[kNumWalls];
+    float wall_angle[kNumWalls];
+    Rot wall_q[kNumWalls];
+    Poly4 cone;
+    // observation key offsets (sorted-key layout); -1 when absent
+    int o_agent, o_bi, o_bim, o_bs, o_bsm, o_box, o_boxm, o_hs, o_hsm, o_heal, o_healm, o_oth, o_othm, o_zone;
+};
+
+// ---------------------------------------------------------------------------
+// select helpers for runtime indices into register arrays
+// ---------------------------------------------------------------------------
+template <int N, class T>
+MAS_HD T sel(const T (&a)[N], int i)
+{
+    T r = opq(a[0]);
+#pragma unroll
+    for (int k = 1; k < N; ++k) r = (i == k) ? opq(a[k]) : r;
+    return r;
+}
+template <int N, class T>
+MAS_HD void put(T (&a)[N], int i, T v)
+{
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if (i == k) a[k] = v;
+}
+
+template <int N, int M, class T>
+MAS_HD T sel2(const T (&a)[N][M], int i, int j)
+{
+    T r = opq(a[0][0]);
+#pragma unroll
+    for (int p = 0; p < N; ++p)
+#pragma unroll
+        for (int q = 0; q < M; ++q) r = (i == p && j == q) ? opq(a[p][q]) : r;
+    return r;
+}
+template <int N, int M, class T>
+MAS_HD void put2(T (&a)[N][M], int i, int j, T v)
+{
+#pragma unroll
+    for (int p = 0; p < N; ++p)
+#pragma unroll
+        for (int q = 0; q < M; ++q)
+            if (i == p && j == q) a[p][q] = v;
+}
+
+// ---------------------------------------------------------------------------
+// env state in registers
+// ---------------------------------------------------------------------------
+template <class C>
+struct EnvL {
+    // agents (slot = IndexBodies id)
+    V2 c[C::AM];
+    float a[C::AM];
+    V2 v[C::AM];
+    float w[C::AM];
+    float sleep[C::AM];
+    uint32_t alive_m, awake_m;
+    int health[C::AM], cause[C::AM], cooldown[C::AM], inv_n[C::AM];
+    int inv_meta[C::AM][C::SM];  // kind | rot<<2 | copied<<4 | (owner+1)<<8
+    float inv_hx[C::AM][C::SM], inv_hy[C::AM][C::SM];
+    // boxes group (list order); meta = rot | copied<<2 | hinit<<3 | (vuln+1)<<8 | (cause+1)<<16
+    int nbox;
+    V2 bp[C::BM];
+    float bhx[C::BM], bhy[C::BM];
+    int bmeta[C::BM], bhealth[C::BM];
+    // box_items group; meta = rot | copied<<2 | (owner+1)<<8
+    int nbi;
+    V2 ip[C::BM];
+    float ihx[C::BM], ihy[C::BM];
+    int imeta[C::BM];
+    // Object.next_spawns (dropped at the next pre_step)
+    int npend;
+    V2 pp[C::BM];
+    float phx[C::BM], phy[C::BM];
+    int pmeta[C::BM];
+    // heals group
+    int nheal;
+    V2 hp[C::HM];
+    // SafeZone
+    V2 zc[kMaxPhases];
+    int phase, t_cd, t_sh, endgame;
+    V2 zpos;
+    float zrad;
+    // contact memory: touching flag + accumulated impulses (b2Manifold points)
+    uint32_t aa_touch;
+    float aa_ni[C::NAA > 0 ? C::NAA : 1], aa_ti[C::NAA > 0 ? C::NAA : 1];
+    uint32_t as_touch[C::AM];
+    float as_ni[C::AM][C::NS], as_ti[C::AM][C::NS];
+    float inv_dt0;
+    // numpy Generator(PCG64) state
+    uint64_t st_hi, st_lo, inc_hi, inc_lo;
+    uint32_t has32, u32v;
+    float stats[kStats];
+};
+
+// visit every persistent word (load / store / count), fixed order
+template <class C, class F>
+MAS_HD void visit_state(EnvL<C>& L, F& f)
+{
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        f.io(L.c[i].x); f.io(L.c[i].y); f.io(L.a[i]); f.io(L.v[i].x); f.io(L.v[i].y); f.io(L.w[i]);
+        f.io(L.sleep[i]); f.io(L.health[i]); f.io(L.cause[i]); f.io(L.cooldown[i]); f.io(L.inv_n[i]);
+#pragma unroll
+        for (int k = 0; k < C::SM; ++k) { f.io(L.inv_meta[i][k]); f.io(L.inv_hx[i][k]); f.io(L.inv_hy[i][k]); }
+    }
+    f.io(L.alive_m); f.io(L.awake_m);
+    f.io(L.nbox); f.io(L.nbi); f.io(L.npend); f.io(L.nheal);
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        f.io(L.bp[b].x); f.io(L.bp[b].y); f.io(L.bhx[b]); f.io(L.bhy[b]); f.io(L.bmeta[b]); f.io(L.bhealth[b]);
+        f.io(L.ip[b].x); f.io(L.ip[b].y); f.io(L.ihx[b]); f.io(L.ihy[b]); f.io(L.imeta[b]);
+        f.io(L.pp[b].x); f.io(L.pp[b].y); f.io(L.phx[b]); f.io(L.phy[b]); f.io(L.pmeta[b]);
+    }
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h) { f.io(L.hp[h].x); f.io(L.hp[h].y); }
+#pragma unroll
+    for (int k = 0; k < kMaxPhases; ++k) { f.io(L.zc[k].x); f.io(L.zc[k].y); }
+    f.io(L.phase); f.io(L.t_cd); f.io(L.t_sh); f.io(L.endgame); f.io(L.zpos.x); f.io(L.zpos.y); f.io(L.zrad);
+    f.io(L.aa_touch);
+#pragma unroll
+    for (int p = 0; p < (C::NAA > 0 ? C::NAA : 1); ++p) { f.io(L.aa_ni[p]); f.io(L.aa_ti[p]); }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        f.io(L.as_touch[i]);
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) { f.io(L.as_ni[i][s]); f.io(L.as_ti[i][s]); }
+    }
+    f.io(L.inv_dt0);
+    f.io64(L.st_hi); f.io64(L.st_lo); f.io64(L.inc_hi); f.io64(L.inc_lo);
+    f.io(L.has32); f.io(L.u32v);
+#pragma unroll
+    for (int k = 0; k < kStats; ++k) f.io(L.stats[k]);
+}
+
+struct WordCounter {
+    int n = 0;
+    template <class T> MAS_HD void io(T&) { n += 1; }
+    template <class T> MAS_HD void io64(T&) { n += 2; }
+};
+
+template <class C>
+inline int state_words()
+{
+    EnvL<C> L;
+    WordCounter wc;
+    visit_state(L, wc);
+    return wc.n;
+}
+
+// ---------------------------------------------------------------------------
+// numpy Generator(PCG64): next64 / next32 / random / random_interval / normal
+// ---------------------------------------------------------------------------
+template <class C>
+MAS_HD uint64_t pcg_next64(EnvL<C>& L)
+{
+    const uint64_t mhi = 0x2360ED051FC65DA4ULL, mlo = 0x4385DF649FCCF645ULL;
+    uint64_t lo = L.st_lo * mlo;
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t hi = __umul64hi(L.st_lo, mlo);
+#else
+    uint64_t hi = (uint64_t)(((unsigned __int128)L.st_lo * mlo) >> 64);
+#endif
+    hi += L.st_lo * mhi + L.st_hi * mlo;
+    uint64_t nlo = lo + L.inc_lo;
+    uint64_t carry = nlo < lo ? 1ULL : 0ULL;
+    L.st_lo = nlo;
+    L.st_hi = hi + L.inc_hi + carry;
+    uint64_t x = L.st_hi ^ L.st_lo;
+    unsigned r = (unsigned)(L.st_hi >> 58);
+    return (x >> r) | (x << ((64u - r) & 63u));
+}
+
+template <class C>
+MAS_HD uint32_t pcg_next32(EnvL<C>& L)
+{
+    if (L.has32) {
+        L.has32 = 0;
+        return L.u32v;
+    }
+    uint64_t n = pcg_next64(L);
+    L.has32 = 1;
+    L.u32v = (uint32_t)(n >> 32);
+    return (uint32_t)(n & 0xffffffffULL);
+}
+
+template <class C>
+MAS_HD double pcg_random(EnvL<C>& L)
+{
+    return (double)(pcg_next64(L) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+template <class C>
+MAS_HD uint32_t pcg_interval32(EnvL<C>& L, uint32_t max)
+{
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    uint32_t v;
+    do {
+        v = pcg_next32(L) & mask;
+    } while (v > max);
+    return v;
+}
+
+template <class C>
+__device__ __forceinline__ double pcg_normal(EnvL<C>& L)
+{
+    for (;;) {
+        uint64_t r = pcg_next64(L);
+        int idx = (int)(r & 0xff);
+        r >>= 8;
+        int sign = (int)(r & 1);
+        uint64_t rabs = (r >> 1) & 0x000fffffffffffffULL;
+        double x = (double)rabs * mas_wi_double[idx];
+        if (sign & 1) x = -x;
+        if (rabs < mas_ki_double[idx]) return x;
+        if (idx == 0) {
+            for (;;) {
+                double xx = -MAS_ZIGGURAT_NOR_INV_R * log1p(-pcg_random(L));
+                double yy = -log1p(-pcg_random(L));
+                if (yy + yy > xx * xx)
+                    return ((rabs >> 8) & 1) ? -(MAS_ZIGGURAT_NOR_R + xx) : MAS_ZIGGURAT_NOR_R + xx;
+            }
+        } else {
+            if (((mas_fi_double[idx - 1] - mas_fi_double[idx]) * pcg_random(L) + mas_fi_double[idx]) <
+                exp(-0.5 * x * x))
+                return x;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+MAS_HD bool bit(uint32_t m, int i) { return (m >> i) & 1u; }
+MAS_HD int team_of(const Params& P, int id) { return id < P.A / 2 ? 0 : 1; }
+MAS_HD int box_rot(int meta) { return meta & 3; }
+MAS_HD int box_copied(int meta) { return (meta >> 2) & 1; }
+MAS_HD int box_hinit(int meta) { return (meta >> 3) & 1; }
+MAS_HD int box_vuln(int meta) { return ((meta >> 8) & 0xff) - 1; }
+MAS_HD int box_cause(int meta) { return ((meta >> 16) & 0xff) - 1; }
+MAS_HD int mk_boxmeta(int rot, int copied, int hinit, int vuln, int cause)
+{
+    return rot | (copied << 2) | (hinit << 3) | ((vuln + 1) << 8) | ((cause + 1) << 16);
+}
+MAS_HD int it_kind(int meta) { return meta & 3; }
+MAS_HD int it_rot(int meta) { return (meta >> 2) & 3; }
+MAS_HD int it_copied(int meta) { return (meta >> 4) & 1; }
+MAS_HD int it_owner(int meta) { return ((meta >> 8) & 0xff) - 1; }
+MAS_HD int mk_itmeta(int kind, int rot, int copied, int owner)
+{
+    return kind | (rot << 2) | (copied << 4) | ((owner + 1) << 8);
+}
+// box-item / pending meta: rot | copied<<2 | (owner+1)<<8
+MAS_HD int bi_rot(int meta) { return meta & 3; }
+MAS_HD int bi_copied(int meta) { return (meta >> 2) & 1; }
+MAS_HD int bi_owner(int meta) { return ((meta >> 8) & 0xff) - 1; }
+MAS_HD int mk_bimeta(int rot, int copied, int owner) { return rot | (copied << 2) | ((owner + 1) << 8); }
+
+constexpr Rot kIdRot = {0.0f, 1.0f};
+
+template <int N>
+MAS_HD int aa_index(int i, int j)
+{
+    // pair (i<j) index in row-major upper-triangle order
+    return i * N - (i * (i + 1)) / 2 + (j - i - 1);
+}
+
+// wake (b2Body::SetAwake(true))
+template <class C>
+MAS_HD void wake(EnvL<C>& L, int i)
+{
+    if (!bit(L.awake_m, i)) {
+        L.awake_m |= 1u << i;
+        put(L.sleep, i, 0.0f);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// static body geometry (walls 0..3, then boxes in list order)
+// ---------------------------------------------------------------------------
+struct StaticG {
+    V2 p;
+    Rot q;
+    float angle;
+    Poly4 poly;
+};
+
+template <class C>
+MAS_HD StaticG static_geom(const EnvL<C>& L, const Params& P, int s)
+{
+    StaticG g;
+    if (s < kNumWalls) {
+        g.p = P.wall_pos[s];
+        g.q = P.wall_q[s];
+        g.angle = P.wall_angle[s];
+        g.poly = P.wall_poly;
+    } else {
+        int b = s - kNumWalls;
+        g.p = L.bp[b];
+        g.q = kIdRot;
+        g.angle = 0.0f;
+        g.poly = box_poly(L.bhx[b], L.bhy[b], box_rot(L.bmeta[b]), box_copied(L.bmeta[b]));
+    }
+    return g;
+}
+
+// runtime static index -> geometry (select)
+template <class C>
+MAS_HD StaticG static_geom_dyn(const EnvL<C>& L, const Params& P, int s)
+{
+    StaticG g = static_geom(L, P, 0);
+#pragma unroll
+    for (int k = 1; k < C::NS; ++k) {
+        if (s == k) g = static_geom(L, P, k);
+    }
+    return g;
+}
+
+}  // namespace mas

@@ -1,0 +1,1243 @@
+// mas_physics.h -- b2World::Step for one env in registers (gfx950 HIP).
+//
+// The world MaSurvival builds is: dynamic circles (agents), static polygons
+// (4 walls + boxes), sensors (heals, box items: no contacts).  Every solver
+// manifold is 1-point (circles or polygon-circle), so the Box2D 2.3.x step
+// reduces to: Collide (narrowphase on every candidate pair, warm-start
+// impulses matched by "touching at the previous update"), island Solve
+// (damping, warm start, 10 sequential-impulse iterations, integrate, <=10
+// position iterations with per-island early exit, sleep) and SolveTOI for
+// agent-vs-static pairs (conservative advancement b2TimeOfImpact + TOI
+// sub-step).  Contacts are kept in a compact per-env list of C::KC register
+// slots in canonical order; an env whose touching-contact count exceeds the
+// slots takes the slow path that walks every candidate pair and recomputes
+// the constraint data each iteration -- same arithmetic, same result.
+#pragma once
+
+#include "mas_env.h"
+
+namespace mas {
+
+constexpr float kBaumgarte = 0.2f;
+constexpr float kToiBaumgarte = 0.75f;
+constexpr float kMaxLinearCorrection = 0.2f;
+constexpr float kMaxTranslation = 2.0f;
+constexpr float kMaxRotation = 0.5f * kPi;
+constexpr float kTimeToSleep = 0.5f;
+constexpr float kLinSleepTol = 0.01f;
+constexpr float kAngSleepTol = 2.0f / 180.0f * kPi;
+
+template <class C>
+struct StepScratch {
+    V2 c0[C::AM];
+    float a0[C::AM];
+};
+
+// ---------------------------------------------------------------------------
+// Collide: b2Contact::Update
+// ---------------------------------------------------------------------------
+template <class C, int I, int J>
+__device__ __forceinline__ void update_aa(EnvL<C>& L, const Params& P)
+{
+    constexpr int p = aa_index<C::AM>(I, J);
+    bool was = bit(L.aa_touch, p);
+    V2 d = sub(L.c[J], L.c[I]);
+    float dsq = dot(d, d);
+    float rad = P.agent_r + P.agent_r;
+    bool touching = !(dsq > rad * rad);
+    if (!(touching && was)) {
+        L.aa_ni[p] = 0.0f;
+        L.aa_ti[p] = 0.0f;
+    }
+    L.aa_touch = touching ? (L.aa_touch | (1u << p)) : (L.aa_touch & ~(1u << p));
+    if (touching != was) {
+        wake(L, I);
+        wake(L, J);
+    }
+}
+
+// polygon(A = static S) vs circle(B = agent I); returns touching, manifold out
+template <class C>
+__device__ __forceinline__ bool update_as_g(EnvL<C>& L, const Params& P, int I, int S, const StaticG& g, V2& ln,
+                                            V2& lp)
+{
+    uint32_t tm = sel(L.as_touch, I);
+    bool was = bit(tm, S);
+    bool touching = collide_pc(g.poly, g.p, g.q, sel(L.c, I), kPolyRadius, P.agent_r, ln, lp);
+    if (!(touching && was)) {
+        put2(L.as_ni, I, S, 0.0f);
+        put2(L.as_ti, I, S, 0.0f);
+    }
+    put(L.as_touch, I, touching ? (tm | (1u << S)) : (tm & ~(1u << S)));
+    if (touching != was) wake(L, I);
+    return touching;
+}
+
+// ---------------------------------------------------------------------------
+// contact constraint (b2ContactSolver, 1-point manifold)
+// ---------------------------------------------------------------------------
+struct VC {
+    V2 normal, rA, rB;
+    float nm, tm, ni, ti;
+};
+
+// InitializeVelocityConstraints for agent-agent (circles, A = i, B = j)
+MAS_HD VC vc_init_aa(V2 cA, V2 cB, float r, float mA, float iA, float mB, float iB)
+{
+    VC k;
+    V2 normal = mk(1.0f, 0.0f);
+    if (dist2(cA, cB) > kEps * kEps) {
+        normal = sub(cB, cA);
+        normalize(normal);
+    }
+    V2 wcA = add(cA, scl(r, normal));
+    V2 wcB = sub(cB, scl(r, normal));
+    V2 point = scl(0.5f, add(wcA, wcB));
+    k.normal = normal;
+    k.rA = sub(point, cA);
+    k.rB = sub(point, cB);
+    float rnA = cross(k.rA, normal), rnB = cross(k.rB, normal);
+    float kn = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+    k.nm = kn > 0.0f ? 1.0f / kn : 0.0f;
+    V2 t = cross_vs(normal, 1.0f);
+    float rtA = cross(k.rA, t), rtB = cross(k.rB, t);
+    float kt = mA + mB + iA * rtA * rtA + iB * rtB * rtB;
+    k.tm = kt > 0.0f ? 1.0f / kt : 0.0f;
+    k.ni = 0.0f;
+    k.ti = 0.0f;
+    return k;
+}
+
+// InitializeVelocityConstraints for static polygon (A) - agent (B), e_faceA
+MAS_HD VC vc_init_as(V2 sp, Rot sq, V2 ln, V2 lp, V2 cB, float rB, float mB, float iB)
+{
+    VC k;
+    V2 normal = rmul(sq, ln);
+    V2 planePoint = xmul(sp, sq, lp);
+    V2 clip = cB;
+    V2 wcA = add(clip, scl(kPolyRadius - dot(sub(clip, planePoint), normal), normal));
+    V2 wcB = sub(clip, scl(rB, normal));
+    V2 point = scl(0.5f, add(wcA, wcB));
+    k.normal = normal;
+    k.rA = sub(point, sp);
+    k.rB = sub(point, cB);
+    const float mA = 0.0f, iA = 0.0f;
+    float rnA = cross(k.rA, normal), rnB = cross(k.rB, normal);
+    float kn = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+    k.nm = kn > 0.0f ? 1.0f / kn : 0.0f;
+    V2 t = cross_vs(normal, 1.0f);
+    float rtA = cross(k.rA, t), rtB = cross(k.rB, t);
+    float kt = mA + mB + iA * rtA * rtA + iB * rtB * rtB;
+    k.tm = kt > 0.0f ? 1.0f / kt : 0.0f;
+    k.ni = 0.0f;
+    k.ti = 0.0f;
+    return k;
+}
+
+// b2ContactSolver::WarmStart for one contact
+MAS_HD void vc_warm(const VC& k, V2& vA, float& wA, V2& vB, float& wB, float mA, float iA, float mB, float iB)
+{
+    V2 t = cross_vs(k.normal, 1.0f);
+    V2 Pi = add(scl(k.ni, k.normal), scl(k.ti, t));
+    wA -= iA * cross(k.rA, Pi);
+    vA = sub(vA, scl(mA, Pi));
+    wB += iB * cross(k.rB, Pi);
+    vB = add(vB, scl(mB, Pi));
+}
+
+// b2ContactSolver::SolveVelocityConstraints for one 1-point contact
+MAS_HD void vc_solve(VC& k, V2& vA, float& wA, V2& vB, float& wB, float mA, float iA, float mB, float iB)
+{
+    V2 t = cross_vs(k.normal, 1.0f);
+    {
+        V2 dv = sub(sub(add(vB, cross_sv(wB, k.rB)), vA), cross_sv(wA, k.rA));
+        float vt = dot(dv, t) - 0.0f;
+        float lambda = k.tm * (-vt);
+        float maxF = 0.2f * k.ni;
+        float ni = clamp_b2(k.ti + lambda, -maxF, maxF);
+        lambda = ni - k.ti;
+        k.ti = ni;
+        V2 Pt = scl(lambda, t);
+        vA = sub(vA, scl(mA, Pt));
+        wA -= iA * cross(k.rA, Pt);
+        vB = add(vB, scl(mB, Pt));
+        wB += iB * cross(k.rB, Pt);
+    }
+    {
+        V2 dv = sub(sub(add(vB, cross_sv(wB, k.rB)), vA), cross_sv(wA, k.rA));
+        float vn = dot(dv, k.normal);
+        float lambda = -k.nm * (vn - 0.0f);
+        float ni = fmax_b2(k.ni + lambda, 0.0f);
+        lambda = ni - k.ni;
+        k.ni = ni;
+        V2 Pn = scl(lambda, k.normal);
+        vA = sub(vA, scl(mA, Pn));
+        wA -= iA * cross(k.rA, Pn);
+        vB = add(vB, scl(mB, Pn));
+        wB += iB * cross(k.rB, Pn);
+    }
+}
+
+// one position-constraint correction; returns the separation measured
+MAS_HD float pc_solve_aa(V2& cA, float& aA, V2& cB, float& aB, float r, float m, float I, float baum)
+{
+    V2 normal = sub(cB, cA);
+    normalize(normal);
+    V2 point = scl(0.5f, add(cA, cB));
+    float sep = dot(sub(cB, cA), normal) - r - r;
+    V2 rA = sub(point, cA), rB = sub(point, cB);
+    float Cc = clamp_b2(baum * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+    float rnA = cross(rA, normal), rnB = cross(rB, normal);
+    float K = m + m + I * rnA * rnA + I * rnB * rnB;
+    float imp = K > 0.0f ? -Cc / K : 0.0f;
+    V2 Pp = scl(imp, normal);
+    cA = sub(cA, scl(m, Pp));
+    aA -= I * cross(rA, Pp);
+    cB = add(cB, scl(m, Pp));
+    aB += I * cross(rB, Pp);
+    return sep;
+}
+
+MAS_HD float pc_solve_as(V2 sp, Rot sq, V2 ln, V2 lp, V2& cB, float& aB, float r, float m, float I, float baum)
+{
+    V2 normal = rmul(sq, ln);
+    V2 planePoint = xmul(sp, sq, lp);
+    V2 clip = cB;
+    float sep = dot(sub(clip, planePoint), normal) - kPolyRadius - r;
+    V2 point = clip;
+    V2 rA = sub(point, sp), rB = sub(point, cB);
+    float Cc = clamp_b2(baum * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+    const float mA = 0.0f, iA = 0.0f;
+    float rnA = cross(rA, normal), rnB = cross(rB, normal);
+    float K = mA + m + iA * rnA * rnA + I * rnB * rnB;
+    float imp = K > 0.0f ? -Cc / K : 0.0f;
+    V2 Pp = scl(imp, normal);
+    cB = add(cB, scl(m, Pp));
+    aB += I * cross(rB, Pp);
+    return sep;
+}
+
+// b2Island::Solve integration with the translation / rotation clamp
+MAS_HD void integrate(V2& c, float& a, V2& v, float& w, float h)
+{
+    V2 tr = scl(h, v);
+    if (dot(tr, tr) > kMaxTranslation * kMaxTranslation) {
+        float ratio = kMaxTranslation / len(tr);
+        v.x *= ratio;
+        v.y *= ratio;
+    }
+    float rot = h * w;
+    if (rot * rot > kMaxRotation * kMaxRotation) {
+        float ratio = kMaxRotation / fabsf(rot);
+        w *= ratio;
+    }
+    c = add(c, scl(h, v));
+    a += h * w;
+}
+
+// ---------------------------------------------------------------------------
+// Solve: islands + compact contact list
+// ---------------------------------------------------------------------------
+template <class C>
+struct Slots {
+    int n;
+    int key[C::KC];  // type<<16 | i<<8 | js   (type 0: agent-agent j; 1: agent-static s)
+    VC k[C::KC];
+    V2 ln[C::KC], lp[C::KC];
+};
+
+MAS_HD int slot_type(int key) { return key >> 16; }
+MAS_HD int slot_i(int key) { return (key >> 8) & 0xff; }
+MAS_HD int slot_js(int key) { return key & 0xff; }
+
+template <class C>
+__device__ __forceinline__ void static_pq(const EnvL<C>& L, const Params& P, int s, V2& sp, Rot& sq)
+{
+    sp = opq(P.wall_pos[0]);
+    sq = P.wall_q[0];
+    sq.s = opq(sq.s);
+    sq.c = opq(sq.c);
+#pragma unroll
+    for (int k = 1; k < kNumWalls; ++k)
+        if (s == k) { sp = opq(P.wall_pos[k]); sq.s = opq(P.wall_q[k].s); sq.c = opq(P.wall_q[k].c); }
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b)
+        if (s == kNumWalls + b) { sp = opq(L.bp[b]); sq = kIdRot; }
+}
+
+template <class C>
+__device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScratch<C>& S, float h, float dtRatio)
+{
+    constexpr int AM = C::AM;
+    const float m = P.inv_mass, I = P.inv_I;
+    // islands over touching agent-agent contacts (Box2D DFS; statics do not propagate)
+    int label[AM];
+#pragma unroll
+    for (int i = 0; i < AM; ++i) label[i] = i;
+#pragma unroll
+    for (int pass = 0; pass < AM; ++pass) {
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = i + 1; j < AM; ++j) {
+                constexpr int dummy = 0;
+                (void)dummy;
+                int p = aa_index<AM>(i, j);
+                if (bit(L.alive_m, i) && bit(L.alive_m, j) && bit(L.aa_touch, p)) {
+                    int l = label[i] < label[j] ? label[i] : label[j];
+                    label[i] = l;
+                    label[j] = l;
+                }
+            }
+    }
+    // solved agents: members of islands with an awake member
+    uint32_t solved = 0;
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < AM; ++j)
+            if (label[j] == label[i] && bit(L.alive_m, j) && bit(L.awake_m, j)) any = true;
+        if (bit(L.alive_m, i) && any) solved |= 1u << i;
+    }
+    if (solved == 0) return;
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+        if (bit(solved, i)) wake(L, i);
+    // sweep start + damping (Pade)
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        if (!bit(solved, i)) continue;
+        S.c0[i] = L.c[i];
+        S.a0[i] = L.a[i];
+        float ld = 1.0f / (1.0f + h * P.lin_damp);
+        L.v[i].x *= ld;
+        L.v[i].y *= ld;
+        float ad = 1.0f / (1.0f + h * P.ang_damp);
+        L.w[i] *= ad;
+    }
+    // compact contact list (canonical order)
+    Slots<C> sl;
+    sl.n = 0;
+    bool overflow = false;
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = i + 1; j < AM; ++j) {
+            int p = aa_index<AM>(i, j);
+            if (bit(solved, i) && bit(solved, j) && bit(L.aa_touch, p)) {
+                if (sl.n < C::KC) {
+                    VC k = vc_init_aa(L.c[i], L.c[j], P.agent_r, m, I, m, I);
+                    k.ni = dtRatio * L.aa_ni[p];
+                    k.ti = dtRatio * L.aa_ti[p];
+                    int key = (0 << 16) | (i << 8) | j;
+#pragma unroll
+                    for (int q = 0; q < C::KC; ++q)
+                        if (q == sl.n) { sl.key[q] = key; sl.k[q] = k; }
+                }
+                sl.n++;
+            }
+        }
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        if (!bit(solved, i)) continue;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (!bit(L.as_touch[i], s)) continue;
+            if (sl.n < C::KC) {
+                StaticG g = static_geom(L, P, s);
+                V2 ln = mk(0.0f, 0.0f), lp = mk(0.0f, 0.0f);
+                collide_pc(g.poly, g.p, g.q, L.c[i], kPolyRadius, P.agent_r, ln, lp);
+                VC k = vc_init_as(g.p, g.q, ln, lp, L.c[i], P.agent_r, m, I);
+                k.ni = dtRatio * L.as_ni[i][s];
+                k.ti = dtRatio * L.as_ti[i][s];
+                int key = (1 << 16) | (i << 8) | s;
+#pragma unroll
+                for (int q = 0; q < C::KC; ++q)
+                    if (q == sl.n) { sl.key[q] = key; sl.k[q] = k; sl.ln[q] = ln; sl.lp[q] = lp; }
+            }
+            sl.n++;
+        }
+    }
+    overflow = sl.n > C::KC;
+    if (!overflow) {
+        // ---------------- fast path: compact slots ----------------
+        // warm start
+#pragma unroll
+        for (int q = 0; q < C::KC; ++q) {
+            if (q >= sl.n) continue;
+            int key = sl.key[q];
+            int i = slot_i(key), js = slot_js(key);
+            V2 vB, vA = mk(0.0f, 0.0f);
+            float wB, wA = 0.0f;
+            if (slot_type(key) == 0) {
+                vA = sel(L.v, i); wA = sel(L.w, i);
+                vB = sel(L.v, js); wB = sel(L.w, js);
+                vc_warm(sl.k[q], vA, wA, vB, wB, m, I, m, I);
+                put(L.v, i, vA); put(L.w, i, wA);
+                put(L.v, js, vB); put(L.w, js, wB);
+            } else {
+                vB = sel(L.v, i); wB = sel(L.w, i);
+                vc_warm(sl.k[q], vA, wA, vB, wB, 0.0f, 0.0f, m, I);
+                put(L.v, i, vB); put(L.w, i, wB);
+            }
+        }
+        for (int it = 0; it < 10; ++it) {
+#pragma unroll
+            for (int q = 0; q < C::KC; ++q) {
+                if (q >= sl.n) continue;
+                int key = sl.key[q];
+                int i = slot_i(key), js = slot_js(key);
+                V2 vB, vA = mk(0.0f, 0.0f);
+                float wB, wA = 0.0f;
+                if (slot_type(key) == 0) {
+                    vA = sel(L.v, i); wA = sel(L.w, i);
+                    vB = sel(L.v, js); wB = sel(L.w, js);
+                    vc_solve(sl.k[q], vA, wA, vB, wB, m, I, m, I);
+                    put(L.v, i, vA); put(L.w, i, wA);
+                    put(L.v, js, vB); put(L.w, js, wB);
+                } else {
+                    vB = sel(L.v, i); wB = sel(L.w, i);
+                    vc_solve(sl.k[q], vA, wA, vB, wB, 0.0f, 0.0f, m, I);
+                    put(L.v, i, vB); put(L.w, i, wB);
+                }
+            }
+        }
+        // store impulses
+#pragma unroll
+        for (int q = 0; q < C::KC; ++q) {
+            if (q >= sl.n) continue;
+            int key = sl.key[q];
+            int i = slot_i(key), js = slot_js(key);
+            if (slot_type(key) == 0) {
+#pragma unroll
+                for (int a = 0; a < AM; ++a)
+#pragma unroll
+                    for (int b = a + 1; b < AM; ++b)
+                        if (a == i && b == js) {
+                            L.aa_ni[aa_index<AM>(a, b)] = sl.k[q].ni;
+                            L.aa_ti[aa_index<AM>(a, b)] = sl.k[q].ti;
+                        }
+            } else {
+#pragma unroll
+                for (int a = 0; a < AM; ++a)
+#pragma unroll
+                    for (int s = 0; s < C::NS; ++s)
+                        if (a == i && s == js) {
+                            L.as_ni[a][s] = sl.k[q].ni;
+                            L.as_ti[a][s] = sl.k[q].ti;
+                        }
+            }
+        }
+    } else {
+        // ---------------- slow path: every candidate pair, recomputed ----------------
+        // (runtime loops, agent / static data through sel/put: this path only
+        // runs for an env with more touching contacts than compact slots)
+        V2 cpos[AM];
+#pragma unroll
+        for (int i = 0; i < AM; ++i) cpos[i] = L.c[i];
+#pragma unroll 1
+        for (int it = -2; it < 10; ++it) {  // -2: scale stored impulses, -1: warm start
+#pragma unroll 1
+            for (int i = 0; i < AM; ++i) {
+#pragma unroll 1
+                for (int j = i + 1; j < AM; ++j) {
+                    int p = aa_index<AM>(i, j);
+                    if (!(bit(solved, i) && bit(solved, j) && bit(L.aa_touch, p))) continue;
+                    float ni = sel(L.aa_ni, p), ti = sel(L.aa_ti, p);
+                    if (it == -2) {
+                        put(L.aa_ni, p, dtRatio * ni);
+                        put(L.aa_ti, p, dtRatio * ti);
+                        continue;
+                    }
+                    VC k = vc_init_aa(sel(cpos, i), sel(cpos, j), P.agent_r, m, I, m, I);
+                    k.ni = ni;
+                    k.ti = ti;
+                    V2 vA = sel(L.v, i), vB = sel(L.v, j);
+                    float wA = sel(L.w, i), wB = sel(L.w, j);
+                    if (it < 0) vc_warm(k, vA, wA, vB, wB, m, I, m, I);
+                    else vc_solve(k, vA, wA, vB, wB, m, I, m, I);
+                    put(L.v, i, vA); put(L.w, i, wA);
+                    put(L.v, j, vB); put(L.w, j, wB);
+                    put(L.aa_ni, p, k.ni);
+                    put(L.aa_ti, p, k.ti);
+                }
+            }
+#pragma unroll 1
+            for (int i = 0; i < AM; ++i) {
+                if (!bit(solved, i)) continue;
+                uint32_t tm = sel(L.as_touch, i);
+#pragma unroll 1
+                for (int s = 0; s < C::NS; ++s) {
+                    if (!bit(tm, s)) continue;
+                    float ni = sel2(L.as_ni, i, s), ti = sel2(L.as_ti, i, s);
+                    if (it == -2) {
+                        put2(L.as_ni, i, s, dtRatio * ni);
+                        put2(L.as_ti, i, s, dtRatio * ti);
+                        continue;
+                    }
+                    StaticG g = static_geom_dyn(L, P, s);
+                    V2 ci = sel(cpos, i);
+                    V2 ln = mk(0.0f, 0.0f), lp = mk(0.0f, 0.0f);
+                    collide_pc(g.poly, g.p, g.q, ci, kPolyRadius, P.agent_r, ln, lp);
+                    VC k = vc_init_as(g.p, g.q, ln, lp, ci, P.agent_r, m, I);
+                    k.ni = ni;
+                    k.ti = ti;
+                    V2 vz = mk(0.0f, 0.0f), vB = sel(L.v, i);
+                    float wz = 0.0f, wB = sel(L.w, i);
+                    if (it < 0) vc_warm(k, vz, wz, vB, wB, 0.0f, 0.0f, m, I);
+                    else vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, I);
+                    put(L.v, i, vB); put(L.w, i, wB);
+                    put2(L.as_ni, i, s, k.ni);
+                    put2(L.as_ti, i, s, k.ti);
+                }
+            }
+        }
+    }
+    // integrate positions
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+        if (bit(solved, i)) integrate(L.c[i], L.a[i], L.v[i], L.w[i], h);
+    // position iterations with per-island early exit
+    uint32_t done_isl = 0;  // bit per island root
+    uint32_t solved_isl = 0;
+    for (int it = 0; it < 10; ++it) {
+        float minsep[AM];
+#pragma unroll
+        for (int r = 0; r < AM; ++r) minsep[r] = 0.0f;
+        if (!overflow) {
+#pragma unroll
+            for (int q = 0; q < C::KC; ++q) {
+                if (q >= sl.n) continue;
+                int key = sl.key[q];
+                int i = slot_i(key), js = slot_js(key);
+                int root = sel(label, i);
+                if (bit(done_isl, root)) continue;
+                float sep;
+                if (slot_type(key) == 0) {
+                    V2 cA = sel(L.c, i), cB = sel(L.c, js);
+                    float aA = sel(L.a, i), aB = sel(L.a, js);
+                    sep = pc_solve_aa(cA, aA, cB, aB, P.agent_r, m, I, kBaumgarte);
+                    put(L.c, i, cA); put(L.a, i, aA);
+                    put(L.c, js, cB); put(L.a, js, aB);
+                } else {
+                    V2 sp;
+                    Rot sq;
+                    static_pq(L, P, js, sp, sq);
+                    V2 cB = sel(L.c, i);
+                    float aB = sel(L.a, i);
+                    sep = pc_solve_as(sp, sq, sl.ln[q], sl.lp[q], cB, aB, P.agent_r, m, I, kBaumgarte);
+                    put(L.c, i, cB); put(L.a, i, aB);
+                }
+#pragma unroll
+                for (int r = 0; r < AM; ++r)
+                    if (r == root) minsep[r] = fmin_b2(minsep[r], sep);
+            }
+        } else {
+#pragma unroll 1
+            for (int i = 0; i < AM; ++i)
+#pragma unroll 1
+                for (int j = i + 1; j < AM; ++j) {
+                    int p = aa_index<AM>(i, j);
+                    if (!(bit(solved, i) && bit(solved, j) && bit(L.aa_touch, p))) continue;
+                    int root = sel(label, i);
+                    if (bit(done_isl, root)) continue;
+                    V2 cA = sel(L.c, i), cB = sel(L.c, j);
+                    float aA = sel(L.a, i), aB = sel(L.a, j);
+                    float sep = pc_solve_aa(cA, aA, cB, aB, P.agent_r, m, I, kBaumgarte);
+                    put(L.c, i, cA); put(L.a, i, aA);
+                    put(L.c, j, cB); put(L.a, j, aB);
+                    put(minsep, root, fmin_b2(sel(minsep, root), sep));
+                }
+#pragma unroll 1
+            for (int i = 0; i < AM; ++i) {
+                if (!bit(solved, i)) continue;
+                uint32_t tm = sel(L.as_touch, i);
+                int root = sel(label, i);
+#pragma unroll 1
+                for (int s = 0; s < C::NS; ++s) {
+                    if (!bit(tm, s) || bit(done_isl, root)) continue;
+                    StaticG g = static_geom_dyn(L, P, s);
+                    V2 ln = mk(0.0f, 0.0f), lp = mk(0.0f, 0.0f);
+                    collide_pc(g.poly, g.p, g.q, sel(S.c0, i), kPolyRadius, P.agent_r, ln, lp);
+                    V2 cB = sel(L.c, i);
+                    float aB = sel(L.a, i);
+                    float sep = pc_solve_as(g.p, g.q, ln, lp, cB, aB, P.agent_r, m, I, kBaumgarte);
+                    put(L.c, i, cB); put(L.a, i, aB);
+                    put(minsep, root, fmin_b2(sel(minsep, root), sep));
+                }
+            }
+        }
+        // islands whose minimum separation is acceptable are done
+        uint32_t all_done = 1;
+#pragma unroll
+        for (int r = 0; r < AM; ++r) {
+            bool is_root = false;
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+                if (bit(solved, i) && label[i] == r) is_root = true;
+            if (!is_root || bit(done_isl, r)) continue;
+            if (minsep[r] >= -3.0f * kLinearSlop) {
+                done_isl |= 1u << r;
+                solved_isl |= 1u << r;
+            } else {
+                all_done = 0;
+            }
+        }
+        if (all_done) break;
+    }
+    // sleep (per island)
+    const float linTolSqr = kLinSleepTol * kLinSleepTol;
+    const float angTolSqr = kAngSleepTol * kAngSleepTol;
+    float minSleep[AM];
+#pragma unroll
+    for (int r = 0; r < AM; ++r) minSleep[r] = kMaxFloat;
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        if (!bit(solved, i)) continue;
+        int r = label[i];
+        float ms = sel(minSleep, r);
+        if (L.w[i] * L.w[i] > angTolSqr || dot(L.v[i], L.v[i]) > linTolSqr) {
+            L.sleep[i] = 0.0f;
+            ms = 0.0f;
+        } else {
+            L.sleep[i] += h;
+            ms = fmin_b2(ms, L.sleep[i]);
+        }
+        put(minSleep, r, ms);
+    }
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        if (!bit(solved, i)) continue;
+        int r = label[i];
+        if (sel(minSleep, r) >= kTimeToSleep && bit(solved_isl, r)) {
+            L.awake_m &= ~(1u << i);
+            L.sleep[i] = 0.0f;
+            L.v[i] = mk(0.0f, 0.0f);
+            L.w[i] = 0.0f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// b2TimeOfImpact: static polygon (A, sweep fixed) vs agent point (B)
+// ---------------------------------------------------------------------------
+struct Sweep {
+    V2 c0, c;
+    float a0, a, alpha0;
+};
+
+struct SVert {
+    V2 wA, wB, w;
+    float a;
+    int iA;
+};
+
+struct ToiPoly {
+    Poly4 P;
+    V2 c;  // static position (c0 == c)
+    float ang;
+};
+
+MAS_HD void sweep_static(const ToiPoly& T, float beta, V2& p, Rot& q)
+{
+    p = add(scl(1.0f - beta, T.c), scl(beta, T.c));
+    float angle = (1.0f - beta) * T.ang + beta * T.ang;
+    q = rot_of(angle);
+}
+
+MAS_HD V2 sweep_point(const Sweep& B, float beta)
+{
+    V2 p = add(scl(1.0f - beta, B.c0), scl(beta, B.c));
+    // xfB.p -= Mul(q, localCenter = 0); the point proxy vertex (0,0) through
+    // the identity-rotation transform: (1*0 - 0*0) + p
+    return mk((1.0f * 0.0f - 0.0f * 0.0f) + p.x, (0.0f * 0.0f + 1.0f * 0.0f) + p.y);
+}
+
+MAS_HD int support4(const Poly4& P, V2 d)
+{
+    int best = 0;
+    float bv = dot(P.v[0], d);
+    for (int i = 1; i < 4; ++i) {
+        float val = dot(P.v[i], d);
+        if (val > bv) { best = i; bv = val; }
+    }
+    return best;
+}
+
+MAS_HD V2 pv(const Poly4& P, int i)
+{
+    V2 r = opq(P.v[0]);
+    for (int k = 1; k < 4; ++k)
+        if (i == k) r = opq(P.v[k]);
+    return r;
+}
+
+struct SCache {
+    float metric;
+    int count;
+    int iA0, iA1;
+};
+
+MAS_HD float simplex_metric(int count, const SVert& v0, const SVert& v1)
+{
+    // count 3 never reaches the cache (overlap -> early exit)
+    return count == 2 ? len(sub(v0.w, v1.w)) : 0.0f;
+}
+
+// b2Distance for polygon (A) vs point (B); returns the distance, updates the cache
+MAS_HD float gjk(SCache& cache, const Poly4& P, V2 pA, Rot qA, V2 pB)
+{
+    SVert v[3];
+    int count = cache.count;
+    for (int k = 0; k < 2; ++k) {
+        if (k < count) {
+            int ia = k == 0 ? cache.iA0 : cache.iA1;
+            v[k].iA = ia;
+            v[k].wA = xmul(pA, qA, pv(P, ia));
+            v[k].wB = pB;
+            v[k].w = sub(v[k].wB, v[k].wA);
+            v[k].a = 0.0f;
+        }
+    }
+    if (count > 1) {
+        float metric1 = cache.metric;
+        float metric2 = simplex_metric(count, v[0], v[1]);
+        if (metric2 < 0.5f * metric1 || 2.0f * metric1 < metric2 || metric2 < kEps) count = 0;
+    }
+    if (count == 0) {
+        v[0].iA = 0;
+        v[0].wA = xmul(pA, qA, P.v[0]);
+        v[0].wB = pB;
+        v[0].w = sub(v[0].wB, v[0].wA);
+        v[0].a = 1.0f;
+        count = 1;
+    }
+    int iter = 0;
+    while (iter < 20) {
+        int saveCount = count;
+        int save0 = v[0].iA, save1 = v[1].iA, save2 = v[2].iA;
+        if (count == 2) {
+            V2 w1 = v[0].w, w2 = v[1].w;
+            V2 e12 = sub(w2, w1);
+            float d12_2 = -dot(w1, e12);
+            if (d12_2 <= 0.0f) {
+                v[0].a = 1.0f;
+                count = 1;
+            } else {
+                float d12_1 = dot(w2, e12);
+                if (d12_1 <= 0.0f) {
+                    v[1].a = 1.0f;
+                    count = 1;
+                    v[0] = v[1];
+                } else {
+                    float inv = 1.0f / (d12_1 + d12_2);
+                    v[0].a = d12_1 * inv;
+                    v[1].a = d12_2 * inv;
+                    count = 2;
+                }
+            }
+        } else if (count == 3) {
+            V2 w1 = v[0].w, w2 = v[1].w, w3 = v[2].w;
+            V2 e12 = sub(w2, w1);
+            float d12_1 = dot(w2, e12), d12_2 = -dot(w1, e12);
+            V2 e13 = sub(w3, w1);
+            float d13_1 = dot(w3, e13), d13_2 = -dot(w1, e13);
+            V2 e23 = sub(w3, w2);
+            float d23_1 = dot(w3, e23), d23_2 = -dot(w2, e23);
+            float n123 = cross(e12, e13);
+            float d123_1 = n123 * cross(w2, w3);
+            float d123_2 = n123 * cross(w3, w1);
+            float d123_3 = n123 * cross(w1, w2);
+            if (d12_2 <= 0.0f && d13_2 <= 0.0f) {
+                v[0].a = 1.0f;
+                count = 1;
+            } else if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) {
+                float inv = 1.0f / (d12_1 + d12_2);
+                v[0].a = d12_1 * inv;
+                v[1].a = d12_2 * inv;
+                count = 2;
+            } else if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) {
+                float inv = 1.0f / (d13_1 + d13_2);
+                v[0].a = d13_1 * inv;
+                v[2].a = d13_2 * inv;
+                count = 2;
+                v[1] = v[2];
+            } else if (d12_1 <= 0.0f && d23_2 <= 0.0f) {
+                v[1].a = 1.0f;
+                count = 1;
+                v[0] = v[1];
+            } else if (d13_1 <= 0.0f && d23_1 <= 0.0f) {
+                v[2].a = 1.0f;
+                count = 1;
+                v[0] = v[2];
+            } else if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) {
+                float inv = 1.0f / (d23_1 + d23_2);
+                v[1].a = d23_1 * inv;
+                v[2].a = d23_2 * inv;
+                count = 2;
+                v[0] = v[2];
+            } else {
+                float inv = 1.0f / (d123_1 + d123_2 + d123_3);
+                v[0].a = d123_1 * inv;
+                v[1].a = d123_2 * inv;
+                v[2].a = d123_3 * inv;
+                count = 3;
+            }
+        }
+        if (count == 3) break;
+        V2 d;
+        if (count == 1) {
+            d = neg(v[0].w);
+        } else {
+            V2 e12 = sub(v[1].w, v[0].w);
+            float sgn = cross(e12, neg(v[0].w));
+            d = sgn > 0.0f ? cross_sv(1.0f, e12) : cross_vs(e12, 1.0f);
+        }
+        if (len2(d) < kEps * kEps) break;
+        SVert nv;
+        nv.iA = support4(P, rmult(qA, neg(d)));
+        nv.wA = xmul(pA, qA, pv(P, nv.iA));
+        nv.wB = pB;
+        nv.w = sub(nv.wB, nv.wA);
+        nv.a = 0.0f;
+        ++iter;
+        bool dup = false;
+        if (saveCount > 0 && nv.iA == save0) dup = true;
+        if (saveCount > 1 && nv.iA == save1) dup = true;
+        if (saveCount > 2 && nv.iA == save2) dup = true;
+        if (dup) break;
+        if (count == 1) v[1] = nv;
+        else v[2] = nv;
+        ++count;
+    }
+    V2 wpA, wpB;
+    if (count == 1) {
+        wpA = v[0].wA;
+        wpB = v[0].wB;
+    } else if (count == 2) {
+        wpA = add(scl(v[0].a, v[0].wA), scl(v[1].a, v[1].wA));
+        wpB = add(scl(v[0].a, v[0].wB), scl(v[1].a, v[1].wB));
+    } else {
+        wpA = add(add(scl(v[0].a, v[0].wA), scl(v[1].a, v[1].wA)), scl(v[2].a, v[2].wA));
+        wpB = wpA;
+    }
+    cache.metric = count == 2 ? len(sub(v[0].w, v[1].w)) : 0.0f;
+    cache.count = count;
+    cache.iA0 = v[0].iA;
+    cache.iA1 = v[1].iA;
+    return len(sub(wpA, wpB));
+}
+
+enum { kToiFailed = 1, kToiOverlapped = 2, kToiTouching = 3, kToiSeparated = 4 };
+
+struct SepFn {
+    int type;  // 0 points, 1 faceA
+    V2 axis, lp;
+};
+
+MAS_HD SepFn sep_init(const SCache& cache, const ToiPoly& T, const Sweep& B, float t1)
+{
+    SepFn f;
+    V2 pA;
+    Rot qA;
+    sweep_static(T, t1, pA, qA);
+    V2 pB = sweep_point(B, t1);
+    if (cache.count == 1) {
+        f.type = 0;
+        V2 pa = xmul(pA, qA, pv(T.P, cache.iA0));
+        f.axis = sub(pB, pa);
+        normalize(f.axis);
+        f.lp = mk(0.0f, 0.0f);
+        return f;
+    }
+    f.type = 1;
+    V2 a1 = pv(T.P, cache.iA0), a2 = pv(T.P, cache.iA1);
+    f.axis = cross_vs(sub(a2, a1), 1.0f);
+    normalize(f.axis);
+    V2 normal = rmul(qA, f.axis);
+    f.lp = scl(0.5f, add(a1, a2));
+    V2 pa = xmul(pA, qA, f.lp);
+    float sv = dot(sub(pB, pa), normal);
+    if (sv < 0.0f) f.axis = neg(f.axis);
+    return f;
+}
+
+MAS_HD float sep_find_min(const SepFn& f, const ToiPoly& T, const Sweep& B, int& iA, float t)
+{
+    V2 pA;
+    Rot qA;
+    sweep_static(T, t, pA, qA);
+    V2 pB = sweep_point(B, t);
+    if (f.type == 0) {
+        V2 axisA = rmult(qA, f.axis);
+        iA = support4(T.P, axisA);
+        V2 pa = xmul(pA, qA, pv(T.P, iA));
+        return dot(sub(pB, pa), f.axis);
+    }
+    V2 normal = rmul(qA, f.axis);
+    V2 pa = xmul(pA, qA, f.lp);
+    iA = -1;
+    return dot(sub(pB, pa), normal);
+}
+
+MAS_HD float sep_eval(const SepFn& f, const ToiPoly& T, const Sweep& B, int iA, float t)
+{
+    V2 pA;
+    Rot qA;
+    sweep_static(T, t, pA, qA);
+    V2 pB = sweep_point(B, t);
+    if (f.type == 0) {
+        V2 pa = xmul(pA, qA, pv(T.P, iA));
+        return dot(sub(pB, pa), f.axis);
+    }
+    V2 normal = rmul(qA, f.axis);
+    V2 pa = xmul(pA, qA, f.lp);
+    return dot(sub(pB, pa), normal);
+}
+
+// b2TimeOfImpact (tMax = 1): static polygon core (radius 0.01) vs point of
+// radius rB.  The static angle is 0 or pi/2, so b2Sweep::Normalize is the
+// identity; the point's angle never reaches its position.
+MAS_HD int time_of_impact(const ToiPoly& T, const Sweep& B, float rB, float& tout)
+{
+    tout = 1.0f;
+    float totalRadius = kPolyRadius + rB;
+    float target = fmax_b2(kLinearSlop, totalRadius - 3.0f * kLinearSlop);
+    float tolerance = 0.25f * kLinearSlop;
+    float t1 = 0.0f;
+    int iter = 0;
+    SCache cache;
+    cache.count = 0;
+    cache.metric = 0.0f;
+    cache.iA0 = 0;
+    cache.iA1 = 0;
+    for (;;) {
+        V2 pA;
+        Rot qA;
+        sweep_static(T, t1, pA, qA);
+        V2 pB = sweep_point(B, t1);
+        float distance = gjk(cache, T.P, pA, qA, pB);
+        if (distance <= 0.0f) {
+            tout = 0.0f;
+            return kToiOverlapped;
+        }
+        if (distance < target + tolerance) {
+            tout = t1;
+            return kToiTouching;
+        }
+        SepFn f = sep_init(cache, T, B, t1);
+        int state = 0;
+        float t2 = 1.0f;
+        int pushBackIter = 0;
+        for (;;) {
+            int iA;
+            float s2 = sep_find_min(f, T, B, iA, t2);
+            if (s2 > target + tolerance) {
+                state = kToiSeparated;
+                tout = 1.0f;
+                break;
+            }
+            if (s2 > target - tolerance) {
+                t1 = t2;
+                break;
+            }
+            float s1 = sep_eval(f, T, B, iA, t1);
+            if (s1 < target - tolerance) {
+                state = kToiFailed;
+                tout = t1;
+                break;
+            }
+            if (s1 <= target + tolerance) {
+                state = kToiTouching;
+                tout = t1;
+                break;
+            }
+            int rootIterCount = 0;
+            float a1 = t1, a2 = t2;
+            for (;;) {
+                float t;
+                if (rootIterCount & 1) t = a1 + (target - s1) * (a2 - a1) / (s2 - s1);
+                else t = 0.5f * (a1 + a2);
+                ++rootIterCount;
+                float sv = sep_eval(f, T, B, iA, t);
+                if (fabsf(sv - target) < tolerance) {
+                    t2 = t;
+                    break;
+                }
+                if (sv > target) {
+                    a1 = t;
+                    s1 = sv;
+                } else {
+                    a2 = t;
+                    s2 = sv;
+                }
+                if (rootIterCount == 50) break;
+            }
+            ++pushBackIter;
+            if (pushBackIter == 8) break;
+        }
+        ++iter;
+        if (state != 0) return state;
+        if (iter == 20) {
+            tout = t1;
+            return kToiFailed;
+        }
+    }
+}
+
+// Conservative pre-test (device only, changes no result): the sweep segment
+// against the polygon core's local rectangle grown by target + tolerance +
+// margin.  b2TimeOfImpact reports "touching" only where the core-to-point
+// distance drops below target + tolerance, so a segment that misses the
+// grown rectangle always yields alpha = 1.
+MAS_HD bool toi_reject(const StaticG& g, V2 p0, V2 p1, float rB)
+{
+    const float R = (kPolyRadius + rB - 3.0f * kLinearSlop) + 0.25f * kLinearSlop + 0.02f;
+    V2 l0 = xmult(g.p, g.q, p0), l1 = xmult(g.p, g.q, p1);
+    float ex = 0.0f, ey = 0.0f;
+    for (int k = 0; k < 4; ++k) {
+        ex = fmaxf(ex, fabsf(g.poly.v[k].x));
+        ey = fmaxf(ey, fabsf(g.poly.v[k].y));
+    }
+    ex += R;
+    ey += R;
+    float tmin = 0.0f, tmax = 1.0f;
+    V2 d = sub(l1, l0);
+    if (fabsf(d.x) < 1e-12f) {
+        if (fabsf(l0.x) > ex) return true;
+    } else {
+        float ta = (-ex - l0.x) / d.x, tb = (ex - l0.x) / d.x;
+        tmin = fmaxf(tmin, fminf(ta, tb));
+        tmax = fminf(tmax, fmaxf(ta, tb));
+        if (tmin > tmax) return true;
+    }
+    if (fabsf(d.y) < 1e-12f) {
+        if (fabsf(l0.y) > ey) return true;
+    } else {
+        float ta = (-ey - l0.y) / d.y, tb = (ey - l0.y) / d.y;
+        tmin = fmaxf(tmin, fminf(ta, tb));
+        tmax = fminf(tmax, fmaxf(ta, tb));
+        if (tmin > tmax) return true;
+    }
+    return false;
+}
+
+// b2World::SolveTOI for agent I (events of different agents are independent:
+// statics never move and agent-agent pairs are not TOI pairs).
+template <class C>
+__device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const StepScratch<C>& S, int I, float dt)
+{
+    const float m = P.inv_mass, Ii = P.inv_I;
+    Sweep sw;
+    sw.c0 = sel(S.c0, I);
+    sw.a0 = sel(S.a0, I);
+    sw.c = sel(L.c, I);
+    sw.a = sel(L.a, I);
+    sw.alpha0 = 0.0f;
+    const int ns = kNumWalls + L.nbox;
+    float toi[C::NS];
+    int cnt[C::NS];
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) { toi[s] = 1.0f; cnt[s] = 0; }
+    uint32_t valid = 0, enabled = 0xffffffffu;
+    for (int guard = 0; guard < 9 * C::NS + 1; ++guard) {
+        // (1) statics whose cached TOI is stale: the conservative pre-test
+        //     settles most of them at alpha = 1 (unrolled, cheap)
+        uint32_t need = 0;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (s >= ns || !bit(enabled, s) || cnt[s] > 8 || bit(valid, s)) continue;
+            StaticG g = static_geom(L, P, s);
+            if (toi_reject(g, sw.c0, sw.c, P.agent_r)) {
+                toi[s] = 1.0f;
+                valid |= 1u << s;
+            } else {
+                need |= 1u << s;
+            }
+        }
+        // (2) full b2TimeOfImpact for the rest (runtime loop: one code copy)
+#pragma unroll 1
+        while (need) {
+            int s = __builtin_ctz(need);
+            need &= need - 1;
+            StaticG g = static_geom_dyn(L, P, s);
+            ToiPoly T;
+            T.P = g.poly;
+            T.c = g.p;
+            T.ang = g.angle;
+            float beta;
+            int st = time_of_impact(T, sw, P.agent_r, beta);
+            float alpha = 1.0f;
+            if (st == kToiTouching) alpha = fmin_b2(sw.alpha0 + (1.0f - sw.alpha0) * beta, 1.0f);
+            put(toi, s, alpha);
+            valid |= 1u << s;
+        }
+        // (3) minimum over the enabled contacts (ties: lowest canonical index)
+        float minAlpha = 1.0f;
+        int minS = -1;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (s >= ns || !bit(enabled, s) || cnt[s] > 8) continue;
+            if (toi[s] < minAlpha) {
+                minAlpha = toi[s];
+                minS = s;
+            }
+        }
+        if (minS < 0 || 1.0f - 10.0f * kEps < minAlpha) break;
+        Sweep backup = sw;
+        {
+            float beta = (minAlpha - sw.alpha0) / (1.0f - sw.alpha0);
+            sw.c0 = add(sw.c0, scl(beta, sub(sw.c, sw.c0)));
+            sw.a0 += beta * (sw.a - sw.a0);
+            sw.alpha0 = minAlpha;
+            sw.c = sw.c0;
+            sw.a = sw.a0;
+        }
+        put(L.c, I, sw.c);
+        put(L.a, I, sw.a);
+        StaticG gm = static_geom_dyn(L, P, minS);
+        V2 lnm = mk(0.0f, 0.0f), lpm = mk(0.0f, 0.0f);
+        bool touching = update_as_g(L, P, I, minS, gm, lnm, lpm);
+        valid &= ~(1u << minS);
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s)
+            if (s == minS) cnt[s] += 1;
+        if (!touching) {
+            enabled &= ~(1u << minS);
+            sw = backup;
+            put(L.c, I, sw.c);
+            put(L.a, I, sw.a);
+            continue;
+        }
+        wake(L, I);
+        // island: the min contact first, then the agent's other touching statics
+        uint32_t isl = 0;
+        V2 iln[C::NS], ilp[C::NS];
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            iln[s] = mk(0.0f, 0.0f);
+            ilp[s] = mk(0.0f, 0.0f);
+            if (s >= ns || s == minS) continue;
+            enabled |= 1u << s;
+            StaticG g = static_geom(L, P, s);
+            if (update_as_g(L, P, I, s, g, iln[s], ilp[s])) isl |= 1u << s;
+        }
+        // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
+        V2 cB = sel(L.c, I);
+        float aB = sel(L.a, I);
+        for (int it = 0; it < 20; ++it) {
+            float minsep = 0.0f;
+            minsep = fmin_b2(minsep, pc_solve_as(gm.p, gm.q, lnm, lpm, cB, aB, P.agent_r, m, Ii, kToiBaumgarte));
+#pragma unroll
+            for (int s = 0; s < C::NS; ++s) {
+                if (!bit(isl, s)) continue;
+                StaticG g = static_geom(L, P, s);
+                minsep = fmin_b2(minsep, pc_solve_as(g.p, g.q, iln[s], ilp[s], cB, aB, P.agent_r, m, Ii, kToiBaumgarte));
+            }
+            if (minsep >= -1.5f * kLinearSlop) break;
+        }
+        sw.c0 = cB;
+        sw.a0 = aB;
+        // ... then 10 velocity iterations without warm starting
+        V2 vB = sel(L.v, I);
+        float wB = sel(L.w, I);
+        float nim = 0.0f, tim = 0.0f;
+        float ni[C::NS], ti[C::NS];
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) { ni[s] = 0.0f; ti[s] = 0.0f; }
+        for (int it = 0; it < 10; ++it) {
+            {
+                VC k = vc_init_as(gm.p, gm.q, lnm, lpm, cB, P.agent_r, m, Ii);
+                k.ni = nim;
+                k.ti = tim;
+                V2 vz = mk(0.0f, 0.0f);
+                float wz = 0.0f;
+                vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                nim = k.ni;
+                tim = k.ti;
+            }
+#pragma unroll
+            for (int s = 0; s < C::NS; ++s) {
+                if (!bit(isl, s)) continue;
+                StaticG g = static_geom(L, P, s);
+                VC k = vc_init_as(g.p, g.q, iln[s], ilp[s], cB, P.agent_r, m, Ii);
+                k.ni = ni[s];
+                k.ti = ti[s];
+                V2 vz = mk(0.0f, 0.0f);
+                float wz = 0.0f;
+                vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                ni[s] = k.ni;
+                ti[s] = k.ti;
+            }
+        }
+        float h = (1.0f - minAlpha) * dt;
+        integrate(cB, aB, vB, wB, h);
+        put(L.c, I, cB);
+        put(L.a, I, aB);
+        put(L.v, I, vB);
+        put(L.w, I, wB);
+        sw.c = cB;
+        sw.a = aB;
+        valid = 0;
+    }
+    put(L.c, I, sw.c);
+    put(L.a, I, sw.a);
+}
+
+// b2World::Step(dt, 10, 10)
+template <class C>
+__device__ __forceinline__ void world_step(EnvL<C>& L, const Params& P, float dt)
+{
+    StepScratch<C> S;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        S.c0[i] = L.c[i];
+        S.a0[i] = L.a[i];
+    }
+    float inv_dt = dt > 0.0f ? 1.0f / dt : 0.0f;
+    float dtRatio = L.inv_dt0 * dt;
+    // Collide: agent-agent pairs, then agent-static pairs (canonical order)
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+#pragma unroll
+        for (int j = i + 1; j < C::AM; ++j) {
+            if (!(bit(L.alive_m, i) && bit(L.alive_m, j))) continue;
+            if (!(bit(L.awake_m, i) || bit(L.awake_m, j))) continue;
+            int p = aa_index<C::AM>(i, j);
+            bool was = bit(L.aa_touch, p);
+            V2 d = sub(L.c[j], L.c[i]);
+            float dsq = dot(d, d);
+            float rad = P.agent_r + P.agent_r;
+            bool touching = !(dsq > rad * rad);
+            if (!(touching && was)) {
+                L.aa_ni[p] = 0.0f;
+                L.aa_ti[p] = 0.0f;
+            }
+            L.aa_touch = touching ? (L.aa_touch | (1u << p)) : (L.aa_touch & ~(1u << p));
+            if (touching != was) {
+                wake(L, i);
+                wake(L, j);
+            }
+        }
+    const int ns = kNumWalls + L.nbox;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (s >= ns) continue;
+            StaticG g = static_geom(L, P, s);
+            V2 ln, lp;
+            update_as_g(L, P, i, s, g, ln, lp);
+        }
+    }
+    world_solve(L, P, S, dt, dtRatio);
+    for (int i = 0; i < C::AM; ++i) {  // runtime loop: toi_agent indexes agents via sel/put
+        if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
+        toi_agent(L, P, S, i, dt);
+    }
+    L.inv_dt0 = inv_dt;
+}
+
+}  // namespace mas

@@ -1,0 +1,976 @@
+// mas_step.h -- MaSurvival rules, observation, reward, done and reset for one
+// env in registers (gfx950 HIP).  Reference: masurvival/semantics.py,
+// simulation.py, envs/masurvival_env.py (cited per block); order of
+// SURVEY.md Appendix A.  Per-thread transient lists (camera candidates,
+// seen-by masks, the spawn-grid permutation) live in LDS, [k][64]-interleaved
+// so that the 64 lanes of a wave hit 64 distinct banks.
+#pragma once
+
+#include "mas_physics.h"
+
+namespace mas {
+
+constexpr int kWG = 64;  // threads (= envs) per workgroup: one wave
+
+// per-thread LDS scratch
+template <class C>
+struct Scr {
+    uint32_t* cand;   // [C::NB][kWG] camera candidates
+    uint32_t* seen;   // [C::NB][kWG] seen-by camera-position bitmask per body
+    uint8_t* perm;    // [256][kWG] spawn-grid permutation
+    int tid;
+    __device__ uint32_t& cd(int k) { return cand[k * kWG + tid]; }
+    __device__ uint32_t& sn(int k) { return seen[k * kWG + tid]; }
+    __device__ uint8_t& pm(int k) { return perm[k * kWG + tid]; }
+};
+
+// unified body index in canonical (dict, then list) order
+template <class C> struct BIdx {
+    static constexpr int box = 0;
+    static constexpr int bitem = C::BM;
+    static constexpr int heal = 2 * C::BM;
+    static constexpr int wall = 2 * C::BM + C::HM;
+    static constexpr int agent = 2 * C::BM + C::HM + kNumWalls;
+};
+
+template <class C>
+__device__ __forceinline__ V2 body_pos(const EnvL<C>& L, const Params& P, int k)
+{
+    V2 r = mk(0.0f, 0.0f);
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (k == BIdx<C>::box + b) r = opq(L.bp[b]);
+        if (k == BIdx<C>::bitem + b) r = opq(L.ip[b]);
+    }
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h)
+        if (k == BIdx<C>::heal + h) r = opq(L.hp[h]);
+#pragma unroll
+    for (int w = 0; w < kNumWalls; ++w)
+        if (k == BIdx<C>::wall + w) r = opq(P.wall_pos[w]);
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+        if (k == BIdx<C>::agent + i) r = opq(L.c[i]);
+    return r;
+}
+
+// simulation.py:431-439 laser_scan + LaserRayCastCallback (:471-484): the
+// closest fixture over ALL fixtures (sensors included); returns the body
+// index or -1.  A report at fraction 0 ends the traversal (b2DynamicTree).
+template <class C>
+__device__ __forceinline__ int ray_cast(const EnvL<C>& L, const Params& P, V2 p1, V2 p2)
+{
+    float maxf = 1.0f;
+    int hit = -1;
+    bool stop = false;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (stop || b >= L.nbox) continue;
+        Poly4 poly = box_poly(L.bhx[b], L.bhy[b], box_rot(L.bmeta[b]), box_copied(L.bmeta[b]));
+        float f = ray_poly(poly, L.bp[b], kIdRot, p1, p2, maxf);
+        if (f >= 0.0f) { hit = BIdx<C>::box + b; maxf = f; stop = maxf == 0.0f; }
+    }
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (stop || b >= L.nbi) continue;
+        float f = ray_circle(P.bitem_r, L.ip[b], p1, p2, maxf);
+        if (f >= 0.0f) { hit = BIdx<C>::bitem + b; maxf = f; stop = maxf == 0.0f; }
+    }
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h) {
+        if (stop || h >= L.nheal) continue;
+        float f = ray_circle(P.heal_r, L.hp[h], p1, p2, maxf);
+        if (f >= 0.0f) { hit = BIdx<C>::heal + h; maxf = f; stop = maxf == 0.0f; }
+    }
+#pragma unroll
+    for (int w = 0; w < kNumWalls; ++w) {
+        if (stop) continue;
+        float f = ray_poly(P.wall_poly, P.wall_pos[w], P.wall_q[w], p1, p2, maxf);
+        if (f >= 0.0f) { hit = BIdx<C>::wall + w; maxf = f; stop = maxf == 0.0f; }
+    }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (stop || !bit(L.alive_m, i)) continue;
+        float f = ray_circle(P.agent_r, L.c[i], p1, p2, maxf);
+        if (f >= 0.0f) { hit = BIdx<C>::agent + i; maxf = f; stop = maxf == 0.0f; }
+    }
+    return hit;
+}
+
+// Cameras._update_seen (simulation.py:336-354): camera list position p =
+// rank among the alive agents; scr.sn(body) gets bit p when body is in the
+// vision cone and the LOS ray to pos + (1+1e-6)*d hits it first.
+template <class C>
+__device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, Scr<C>& scr)
+{
+#pragma unroll
+    for (int k = 0; k < C::NB; ++k) scr.sn(k) = 0u;
+    int p = 0;
+    for (int i = 0; i < C::AM; ++i) {
+        if (!bit(L.alive_m, i)) continue;
+        V2 pos = sel(L.c, i);
+        Rot q = rot_of(sel(L.a, i));
+        int nc = 0;
+#pragma unroll
+        for (int b = 0; b < C::BM; ++b)
+            if (b < L.nbox && poly_test_point(P.cone, pos, q, L.bp[b])) scr.cd(nc++) = BIdx<C>::box + b;
+#pragma unroll
+        for (int b = 0; b < C::BM; ++b)
+            if (b < L.nbi && poly_test_point(P.cone, pos, q, L.ip[b])) scr.cd(nc++) = BIdx<C>::bitem + b;
+#pragma unroll
+        for (int h = 0; h < C::HM; ++h)
+            if (h < L.nheal && poly_test_point(P.cone, pos, q, L.hp[h])) scr.cd(nc++) = BIdx<C>::heal + h;
+#pragma unroll
+        for (int w = 0; w < kNumWalls; ++w)
+            if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) scr.cd(nc++) = BIdx<C>::wall + w;
+#pragma unroll
+        for (int j = 0; j < C::AM; ++j)
+            if (j != i && bit(L.alive_m, j) && poly_test_point(P.cone, pos, q, L.c[j]))
+                scr.cd(nc++) = BIdx<C>::agent + j;
+        const float eps1 = (float)(1.0 + 1e-6);
+        for (int k = 0; k < nc; ++k) {
+            int body = (int)scr.cd(k);
+            V2 oc = body_pos(L, P, body);
+            V2 d = sub(oc, pos);
+            V2 end = add(pos, scl(eps1, d));
+            int hit = ray_cast(L, P, pos, end);
+            if (hit == body) scr.sn(body) |= 1u << p;
+        }
+        ++p;
+    }
+}
+
+// Health._change_health for agents (semantics.py:490-500); teammates are
+// immune to their own badge (TwoTeams.post_reset :942-946)
+template <class C>
+__device__ __forceinline__ void agent_damage(EnvL<C>& L, const Params& P, int t, int delta, int cause)
+{
+    if (!bit(L.alive_m, t)) return;
+    if (P.teams && cause == kCauseBadge + team_of(P, t)) return;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+        if (i == t) {
+            L.health[i] += delta;
+            L.cause[i] = cause;
+        }
+}
+
+template <class C>
+__device__ __forceinline__ void box_damage(EnvL<C>& L, int b, int delta, int cause)
+{
+#pragma unroll
+    for (int k = 0; k < C::BM; ++k) {
+        if (k != b) continue;
+        int meta = L.bmeta[k];
+        if (!box_hinit(meta)) continue;  // not in Health.healths yet
+        int vuln = box_vuln(meta);
+        if (vuln != kCauseNone && cause != vuln) continue;  // OwnedObjectItem vulnerabilities
+        L.bhealth[k] += delta;
+        L.bmeta[k] = mk_boxmeta(box_rot(meta), box_copied(meta), 1, vuln, cause);
+    }
+}
+
+// Inventory.take of one item (semantics.py:179-187) into agent t (runtime)
+template <class C>
+__device__ __forceinline__ bool inv_take(EnvL<C>& L, const Params& P, int t, int meta, float hx, float hy)
+{
+    bool ok = false;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (i != t) continue;
+        if (1 + L.inv_n[i] > P.slots) continue;
+#pragma unroll
+        for (int k = 0; k < C::SM; ++k)
+            if (k == L.inv_n[i]) {
+                L.inv_meta[i][k] = meta;
+                L.inv_hx[i][k] = hx;
+                L.inv_hy[i][k] = hy;
+            }
+        L.inv_n[i] += 1;
+        ok = true;
+    }
+    return ok;
+}
+
+// pop the last inventory item of agent i (static i)
+template <class C>
+__device__ __forceinline__ void inv_pop(EnvL<C>& L, int i, int& meta, float& hx, float& hy)
+{
+    int n = L.inv_n[i] - 1;
+    meta = sel(L.inv_meta[i], n);
+    hx = sel(L.inv_hx[i], n);
+    hy = sel(L.inv_hy[i], n);
+    L.inv_n[i] = n;
+}
+
+template <class C>
+__device__ __forceinline__ void spawn_box(EnvL<C>& L, const Params& P, V2 pos, float hx, float hy, int rot,
+                                          int copied, int vuln)
+{
+    int nb = L.nbox;
+    if (nb >= C::BM) return;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (b != nb) continue;
+        L.bp[b] = pos;
+        L.bhx[b] = hx;
+        L.bhy[b] = hy;
+        L.bmeta[b] = mk_boxmeta(rot, copied, 0, vuln, kCauseNone);
+        L.bhealth[b] = 0;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            L.as_touch[i] &= ~(1u << (kNumWalls + b));
+            L.as_ni[i][kNumWalls + b] = 0.0f;
+            L.as_ti[i][kNumWalls + b] = 0.0f;
+        }
+    }
+    L.nbox = nb + 1;
+}
+
+template <class C>
+__device__ __forceinline__ void spawn_bitem(EnvL<C>& L, V2 pos, float hx, float hy, int meta)
+{
+    int n = L.nbi;
+    if (n >= C::BM) return;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b)
+        if (b == n) {
+            L.ip[b] = pos;
+            L.ihx[b] = hx;
+            L.ihy[b] = hy;
+            L.imeta[b] = meta;
+        }
+    L.nbi = n + 1;
+}
+
+template <class C>
+__device__ __forceinline__ void spawn_heal(EnvL<C>& L, V2 pos)
+{
+    int n = L.nheal;
+    if (n >= C::HM) return;
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h)
+        if (h == n) L.hp[h] = pos;
+    L.nheal = n + 1;
+}
+
+// ---------------------------------------------------------------------------
+// observation row writer: fetch_observations (masurvival_env.py:510-657)
+// ---------------------------------------------------------------------------
+template <class C>
+__device__ __forceinline__ void write_obs(const EnvL<C>& L, const Params& P, Scr<C>& scr, float* __restrict__ obs_env)
+{
+    const int A = P.A, D = P.D, as_ = P.as_;
+    int post_pos[C::AM];
+    int np = 0;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        post_pos[i] = bit(L.alive_m, i) ? np : -1;
+        np += bit(L.alive_m, i) ? 1 : 0;
+    }
+    float zone6[6];
+    zone6[0] = L.zpos.x;
+    zone6[1] = L.zpos.y;
+    zone6[2] = L.zrad;
+    zone6[3] = 0.0f;
+    zone6[4] = 0.0f;
+    zone6[5] = 0.0f;
+    if (L.phase < P.zone_phases - 1) {
+        int ph = L.phase + 1;
+        zone6[3] = sel(L.zc, ph).x;
+        zone6[4] = sel(L.zc, ph).y;
+#pragma unroll
+        for (int k = 0; k < kMaxPhases; ++k)
+            if (k == ph) zone6[5] = opq(P.zradf[k]);
+    }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (i >= A) continue;
+        float* row = obs_env + (size_t)i * D;
+        bool alive = bit(L.alive_m, i);
+        int pp = post_pos[i];
+        // agent + others rows (_fetch_agents_observations :659-704)
+#pragma unroll
+        for (int j = 0; j < C::AM; ++j) {
+            if (j >= A) continue;
+            float r[9];
+            int k = 0;
+            r[k++] = (float)j;
+            if (P.teams) r[k++] = (float)team_of(P, j);
+            bool aj = bit(L.alive_m, j);
+            r[k++] = aj ? (float)L.health[j] : 0.0f;
+            r[k++] = aj ? L.c[j].x : 0.0f;
+            r[k++] = aj ? L.c[j].y : 0.0f;
+            r[k++] = aj ? L.a[j] : 0.0f;
+            r[k++] = aj ? L.v[j].x : 0.0f;
+            r[k++] = aj ? L.v[j].y : 0.0f;
+            r[k++] = aj ? L.w[j] : 0.0f;
+            int base;
+            if (j == i) base = P.o_agent;
+            else base = P.o_oth + (j < i ? j : j - 1) * as_;
+            for (int q = 0; q < as_; ++q) row[base + q] = r[q];
+            if (j != i) {
+                // others_mask: seen list at the post-despawn list index (quirk D1)
+                float m = 1.0f;
+                if (alive && aj && (scr.sn(BIdx<C>::agent + j) >> pp) & 1u) m = 0.0f;
+                row[P.o_othm + (j < i ? j : j - 1)] = m;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) row[P.o_zone + q] = zone6[q];
+        if (P.H > 0) {
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h) {
+                if (h >= P.H) continue;
+                bool present = h < L.nheal;
+                row[P.o_heal + 2 * h] = present ? L.hp[h].x : 0.0f;
+                row[P.o_heal + 2 * h + 1] = present ? L.hp[h].y : 0.0f;
+                float m;
+                if (P.omniscient) m = present ? 0.0f : 1.0f;
+                else m = (present && alive && ((scr.sn(BIdx<C>::heal + h) >> pp) & 1u)) ? 0.0f : 1.0f;
+                row[P.o_healm + h] = m;
+            }
+        }
+        if (P.B > 0) {
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b) {
+                if (b >= P.B) continue;
+                bool present = b < L.nbox;
+                Poly4 poly = box_poly(L.bhx[b], L.bhy[b], box_rot(L.bmeta[b]), box_copied(L.bmeta[b]));
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    row[P.o_box + 11 * b + 2 * v] = present ? poly.v[v].x : 0.0f;
+                    row[P.o_box + 11 * b + 2 * v + 1] = present ? poly.v[v].y : 0.0f;
+                }
+                row[P.o_box + 11 * b + 8] = present ? L.bp[b].x : 0.0f;
+                row[P.o_box + 11 * b + 9] = present ? L.bp[b].y : 0.0f;
+                row[P.o_box + 11 * b + 10] = 0.0f;  // box bodies always have angle 0
+                float m;
+                if (P.omniscient) m = present ? 0.0f : 1.0f;
+                else m = (present && alive && ((scr.sn(BIdx<C>::box + b) >> pp) & 1u)) ? 0.0f : 1.0f;
+                row[P.o_boxm + b] = m;
+            }
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b) {
+                if (b >= P.B) continue;
+                bool present = b < L.nbi;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    V2 cv = box_corner(L.ihx[b], L.ihy[b], bi_rot(L.imeta[b]) + v);
+                    row[P.o_bi + 10 * b + 2 * v] = present ? cv.x : 0.0f;
+                    row[P.o_bi + 10 * b + 2 * v + 1] = present ? cv.y : 0.0f;
+                }
+                row[P.o_bi + 10 * b + 8] = present ? L.ip[b].x : 0.0f;
+                row[P.o_bi + 10 * b + 9] = present ? L.ip[b].y : 0.0f;
+                float m;
+                if (P.omniscient) m = present ? 0.0f : 1.0f;
+                else m = (present && alive && ((scr.sn(BIdx<C>::bitem + b) >> pp) & 1u)) ? 0.0f : 1.0f;
+                row[P.o_bim + b] = m;
+            }
+        }
+        // usable inventory slots (:620-654)
+        int lastmeta = 0;
+        float lhx = 0.0f, lhy = 0.0f;
+        if (alive && L.inv_n[i] > 0) {
+            int n = L.inv_n[i] - 1;
+            lastmeta = sel(L.inv_meta[i], n);
+            lhx = sel(L.inv_hx[i], n);
+            lhy = sel(L.inv_hy[i], n);
+        }
+        if (P.H > 0) {
+            bool isheal = it_kind(lastmeta) == kItemHeal;
+            row[P.o_hs] = isheal ? (float)P.healing : 0.0f;
+            row[P.o_hsm] = isheal ? 0.0f : 1.0f;
+        }
+        if (P.B > 0) {
+            bool isbox = it_kind(lastmeta) == kItemBox;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                V2 cv = box_corner(lhx, lhy, it_rot(lastmeta) + v);
+                row[P.o_bs + 2 * v] = isbox ? cv.x : 0.0f;
+                row[P.o_bs + 2 * v + 1] = isbox ? cv.y : 0.0f;
+            }
+            row[P.o_bsm] = isbox ? 0.0f : 1.0f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// reset: BaseEnv.reset (masurvival_env.py:59-74) -> Simulation.reset
+// ---------------------------------------------------------------------------
+template <class C>
+__device__ __forceinline__ void env_reset(EnvL<C>& L, const Params& P, Scr<C>& scr)
+{
+    const int A = P.A, H = P.H, B = P.B;
+    const int g = P.grid_size;
+    const int n = g * g;
+    // SpawnGrid.reset: shuffle(square_grid) (semantics.py:71-74, 987-992)
+    for (int k = 0; k < n; ++k) scr.pm(k) = (uint8_t)k;
+    for (int i = n - 1; i >= 1; --i) {
+        int j = (int)pcg_interval32(L, (uint32_t)i);
+        uint8_t t = scr.pm(i);
+        scr.pm(i) = scr.pm(j);
+        scr.pm(j) = t;
+    }
+    int top = n;
+    auto cell = [&](int k) -> V2 {
+        int ii = k % g, jj = k / g;
+        double ci = (double)ii / g + 0.5 / g;
+        double cj = (double)jj / g + 0.5 / g;
+        ci = P.floor_size * ci - P.floor_size / 2.0;
+        cj = P.floor_size * cj - P.floor_size / 2.0;
+        return mk((float)ci, (float)cj);
+    };
+    // new b2World: no contacts, inv_dt0 = 0
+    L.aa_touch = 0;
+#pragma unroll
+    for (int p = 0; p < (C::NAA > 0 ? C::NAA : 1); ++p) { L.aa_ni[p] = 0.0f; L.aa_ti[p] = 0.0f; }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        L.as_touch[i] = 0;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) { L.as_ni[i][s] = 0.0f; L.as_ti[i][s] = 0.0f; }
+    }
+    L.inv_dt0 = 0.0f;
+    // boxes: RandomizeBoxShapes (semantics.py:107-120), ResetSpawns, Health
+    L.nbox = 0;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        L.bp[b] = mk(0.0f, 0.0f);
+        L.bhx[b] = 0.0f;
+        L.bhy[b] = 0.0f;
+        L.bmeta[b] = mk_boxmeta(0, 0, 0, kCauseNone, kCauseNone);
+        L.bhealth[b] = 0;
+        if (b >= B) continue;
+        float hx = P.box_hx, hy = P.box_hy;
+        if (P.randomized) {
+            double wv = P.avg_w + P.std_w * pcg_normal(L);
+            wv = P.min_w > wv ? P.min_w : wv;
+            double hv = P.avg_h + P.std_h * pcg_normal(L);
+            hv = P.min_h > hv ? P.min_h : hv;
+            hx = (float)(wv / 2.0);
+            hy = (float)(hv / 2.0);
+        }
+        L.bhx[b] = hx;
+        L.bhy[b] = hy;
+    }
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (b >= B) continue;
+        L.bp[b] = cell(scr.pm(--top));
+        L.bmeta[b] = mk_boxmeta(0, 0, 1, kCauseNone, kCauseNone);
+        L.bhealth[b] = P.box_health;
+        L.nbox = b + 1;
+    }
+    L.nbi = 0;
+    L.npend = 0;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        L.ip[b] = mk(0.0f, 0.0f); L.ihx[b] = 0.0f; L.ihy[b] = 0.0f; L.imeta[b] = 0;
+        L.pp[b] = mk(0.0f, 0.0f); L.phx[b] = 0.0f; L.phy[b] = 0.0f; L.pmeta[b] = 0;
+    }
+    L.nheal = 0;
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h) {
+        L.hp[h] = mk(0.0f, 0.0f);
+        if (h >= H) continue;
+        L.hp[h] = cell(scr.pm(--top));
+        L.nheal = h + 1;
+    }
+    L.alive_m = 0;
+    L.awake_m = 0;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        L.c[i] = mk(0.0f, 0.0f);
+        L.a[i] = 0.0f;
+        L.v[i] = mk(0.0f, 0.0f);
+        L.w[i] = 0.0f;
+        L.sleep[i] = 0.0f;
+        L.health[i] = 0;
+        L.cause[i] = kCauseNone;
+        L.cooldown[i] = 0;
+        L.inv_n[i] = 0;
+#pragma unroll
+        for (int k = 0; k < C::SM; ++k) { L.inv_meta[i][k] = 0; L.inv_hx[i][k] = 0.0f; L.inv_hy[i][k] = 0.0f; }
+        if (i >= A) continue;
+        L.c[i] = cell(scr.pm(--top));
+        L.alive_m |= 1u << i;
+        L.awake_m |= 1u << i;
+        L.health[i] = P.agent_health;
+    }
+    // SafeZone.post_reset (semantics.py:739-756)
+    const int nr = P.zone_nr;
+#pragma unroll
+    for (int k = 0; k < kMaxPhases; ++k) L.zc[k] = mk(0.0f, 0.0f);
+    if (P.zone_random) {
+        for (int k = nr; k >= 0; --k) {
+            double r = 0.0;
+#pragma unroll
+            for (int q = 0; q < kMaxPhases; ++q)
+                if (q == k) r = opq(P.zrad[q]);
+            double Lz = P.floor_size - 2.0 * r;
+            double cx = (pcg_random(L) * Lz) - Lz / 2.0;
+            double cy = (pcg_random(L) * Lz) - Lz / 2.0;
+            put(L.zc, k, mk((float)cx, (float)cy));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMaxPhases; ++k)
+            if (k < nr) L.zc[k] = mk(P.zfix[k][0], P.zfix[k][1]);
+    }
+    L.t_cd = P.zone_cooldown;
+    L.t_sh = 0;
+    L.phase = 0;
+    L.endgame = 0;
+    L.zpos = L.zc[0];
+    L.zrad = P.zradf[0];
+}
+
+// SafeZone.tick (semantics.py:776-811)
+template <class C>
+__device__ __forceinline__ void zone_tick(EnvL<C>& L, const Params& P)
+{
+    if (L.t_cd == 0) {
+        if (L.endgame) return;
+        L.t_sh -= 1;
+        if (L.t_sh > 0) {
+            double t = (double)L.t_sh / (double)P.zone_cooldown;
+            double r1 = 0.0, r2 = 0.0;
+#pragma unroll
+            for (int k = 0; k + 1 < kMaxPhases; ++k)
+                if (k == L.phase) { r1 = opq(P.zrad[k]); r2 = opq(P.zrad[k + 1]); }
+            V2 c1 = sel(L.zc, L.phase), c2 = sel(L.zc, L.phase + 1);
+            double radius = t * r1 + (1.0 - t) * r2;
+            float tf = (float)t, tf1 = (float)(1.0 - t);
+            L.zrad = (float)radius;
+            L.zpos = add(scl(tf, c1), scl(tf1, c2));
+            return;
+        }
+        L.t_cd = P.zone_cooldown;
+        L.phase += 1;
+        L.zpos = sel(L.zc, L.phase);
+#pragma unroll
+        for (int k = 0; k < kMaxPhases; ++k)
+            if (k == L.phase) L.zrad = opq(P.zradf[k]);
+        if (L.phase == P.zone_phases - 1) L.endgame = 1;
+    } else {
+        L.t_cd -= 1;
+        if (L.t_cd > 0) return;
+        L.t_sh = P.zone_cooldown;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// one env step: BaseEnv.step (masurvival_env.py:76-90)
+// ---------------------------------------------------------------------------
+template <class C>
+__device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& scr, const int8_t* __restrict__ act, float* rew)
+{
+    const int A = P.A;
+    // queue_actions (masurvival_env.py:741-755): alive agents only
+    int ac[C::AM][6];
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            int x = i < A ? (int)act[i * 6 + k] : 0;
+            int hi = k < 3 ? 2 : 1;
+            ac[i][k] = x < 0 ? 0 : (x > hi ? hi : x);
+        }
+    // ---------------- pre_step ----------------
+    // boxes: Object.pre_step drops last step's queued box items (semantics.py:853-856)
+#pragma unroll
+    for (int k = 0; k < C::BM; ++k)
+        if (k < L.npend) spawn_bitem(L, L.pp[k], L.phx[k], L.phy[k], L.pmeta[k]);
+    L.npend = 0;
+    // agents: DynamicMotors (simulation.py:407-424)
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!bit(L.alive_m, i)) continue;
+        Rot q = rot_of(L.a[i]);
+        float par = (float)(ac[i][0] - 1) * P.imp0;
+        float nor = (float)(ac[i][1] - 1) * P.imp1;
+        V2 J = mk(q.c * par + (-q.s) * nor, q.s * par + q.c * nor);
+        float ang = (float)(ac[i][2] - 1) * P.imp2;
+        wake(L, i);
+        L.v[i] = add(L.v[i], scl(P.inv_mass, J));
+        L.w[i] += P.inv_I * cross(sub(L.c[i], L.c[i]), J);
+        L.w[i] += P.inv_I * ang;
+    }
+    // UseLast (semantics.py:300-309): Heal.use (:646-649) / ObjectItem.use (:830-836)
+    int uses_heal = 0, uses_box = 0;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!bit(L.alive_m, i) || !ac[i][4] || L.inv_n[i] == 0) continue;
+        int meta;
+        float hx, hy;
+        inv_pop(L, i, meta, hx, hy);
+        if (it_kind(meta) == kItemHeal) {
+            uses_heal++;
+            agent_damage(L, P, i, P.healing, kCauseNone);
+        } else if (it_kind(meta) == kItemBox) {
+            uses_box++;
+            V2 off = from_polar(P.box_item_offset, L.a[i]);
+            spawn_box(L, P, add(L.c[i], off), hx, hy, it_rot(meta), it_copied(meta),
+                      P.ownership ? it_owner(meta) : kCauseNone);
+        }
+    }
+    // GiveLast (semantics.py:335-370): nearest body centre within the give radius
+    {
+        int taker[C::AM];
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            taker[i] = -1;
+            if (!bit(L.alive_m, i)) continue;
+            V2 c = L.c[i];
+            float mind = INFINITY;
+            int best = -1;
+            auto consider = [&](V2 oc, int id) {
+                if (!circle_test_point(P.give_r, c, oc)) return;
+                float dd = len(sub(c, oc));
+                if (dd < mind) { mind = dd; best = id; }
+            };
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b)
+                if (b < L.nbox) consider(L.bp[b], BIdx<C>::box + b);
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b)
+                if (b < L.nbi) consider(L.ip[b], BIdx<C>::bitem + b);
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h)
+                if (h < L.nheal) consider(L.hp[h], BIdx<C>::heal + h);
+#pragma unroll
+            for (int w = 0; w < kNumWalls; ++w) consider(P.wall_pos[w], BIdx<C>::wall + w);
+#pragma unroll
+            for (int j = 0; j < C::AM; ++j)
+                if (j != i && bit(L.alive_m, j)) consider(L.c[j], BIdx<C>::agent + j);
+            taker[i] = best;
+        }
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            if (!bit(L.alive_m, i) || !ac[i][5] || taker[i] < BIdx<C>::agent) continue;
+            int t = taker[i] - BIdx<C>::agent;
+            if (P.teams && team_of(P, t) != team_of(P, i)) continue;  // strangers
+            if (L.inv_n[i] == 0) continue;
+            int meta;
+            float hx, hy;
+            inv_pop(L, i, meta, hx, hy);
+            inv_take(L, P, t, meta, hx, hy);  // full inventory: the item is lost (quirk D3)
+        }
+    }
+    // Melee / ContinuousMelee (semantics.py:531-554, 584-610): all rays first
+    {
+        int target[C::AM];
+        for (int i = 0; i < C::AM; ++i) {
+            int tg = -1;
+            if (bit(L.alive_m, i)) {
+                V2 c = sel(L.c, i);
+                V2 hand = from_polar(P.melee_range, sel(L.a, i));
+                tg = ray_cast(L, P, c, add(c, hand));
+            }
+            put(target, i, tg);
+        }
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            if (!bit(L.alive_m, i)) continue;
+            bool on_cd = P.melee_cd > 0 && L.cooldown[i] > 0;
+            if (target[i] >= 0 && ac[i][3] && !on_cd) {
+                int cause = P.teams ? kCauseBadge + team_of(P, i) : i;
+                int tg = target[i];
+                if (tg >= BIdx<C>::agent) agent_damage(L, P, tg - BIdx<C>::agent, -P.melee_damage, cause);
+                else if (tg < BIdx<C>::bitem) box_damage(L, tg, -P.melee_damage, cause);
+                if (P.melee_cd > 0) L.cooldown[i] = P.melee_cd;
+            }
+        }
+        if (P.melee_cd > 0) {
+#pragma unroll
+            for (int i = 0; i < C::AM; ++i)
+                if (L.cooldown[i] > 0) L.cooldown[i] -= 1;
+        }
+    }
+    // ---------------- physics: 2 x world.Step(1/60, 10, 10) ----------------
+    const float dt = (float)(1.0 / 60.0);
+    world_step(L, P, dt);
+    world_step(L, P, dt);
+    // ---------------- post_step ----------------
+    // boxes: Health.post_step + Object / OwnedObject despawn (semantics.py:429-435, 858-861, 907-912)
+    {
+        bool any_dead = false;
+#pragma unroll
+        for (int b = 0; b < C::BM; ++b) {
+            if (b >= L.nbox) continue;
+            int meta = L.bmeta[b];
+            if (!box_hinit(meta)) {
+                L.bmeta[b] = mk_boxmeta(box_rot(meta), box_copied(meta), 1, box_vuln(meta), box_cause(meta));
+                L.bhealth[b] = P.box_health;
+            }
+            if (L.bhealth[b] <= 0) any_dead = true;
+        }
+        if (any_dead) {
+            // stable compaction; dead boxes queue (pos, copy_shape(proto), cause)
+            int wi = 0;
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b) {
+                if (b >= L.nbox) continue;
+                V2 p = L.bp[b];
+                float hx = L.bhx[b], hy = L.bhy[b];
+                int meta = L.bmeta[b], hl = L.bhealth[b];
+                if (hl <= 0) {
+                    int rot = box_copy_rot(hx, hy, box_rot(meta));
+                    int pm = mk_bimeta(rot, 1, box_cause(meta));
+                    int np_ = L.npend;
+#pragma unroll
+                    for (int k = 0; k < C::BM; ++k)
+                        if (k == np_) { L.pp[k] = p; L.phx[k] = hx; L.phy[k] = hy; L.pmeta[k] = pm; }
+                    L.npend = np_ + 1;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < C::BM; ++k) {
+                        if (k != wi || k > b) continue;
+                        L.bp[k] = p; L.bhx[k] = hx; L.bhy[k] = hy; L.bmeta[k] = meta; L.bhealth[k] = hl;
+#pragma unroll
+                        for (int i = 0; i < C::AM; ++i) {
+                            bool tb = bit(L.as_touch[i], kNumWalls + b);
+                            L.as_touch[i] = tb ? (L.as_touch[i] | (1u << (kNumWalls + k)))
+                                               : (L.as_touch[i] & ~(1u << (kNumWalls + k)));
+                            L.as_ni[i][kNumWalls + k] = L.as_ni[i][kNumWalls + b];
+                            L.as_ti[i][kNumWalls + k] = L.as_ti[i][kNumWalls + b];
+                        }
+                    }
+                    ++wi;
+                }
+            }
+            L.nbox = wi;
+#pragma unroll
+            for (int k = 0; k < C::BM; ++k) {
+                if (k < wi) continue;
+#pragma unroll
+                for (int i = 0; i < C::AM; ++i) {
+                    L.as_touch[i] &= ~(1u << (kNumWalls + k));
+                    L.as_ni[i][kNumWalls + k] = 0.0f;
+                    L.as_ti[i][kNumWalls + k] = 0.0f;
+                }
+            }
+        }
+    }
+    // agents: Cameras.post_step over the pre-despawn list
+    update_seen(L, P, scr);
+    // agents: Health.post_step -> despawn dead (id order): TrackDeaths, IndexBodies,
+    // DeathDrop (semantics.py:387-396), Inventory, Health.pre_despawn -> TrackKills
+    uint32_t died = 0;
+    int kill_cause[C::AM];
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        kill_cause[i] = kCauseNone;
+        if (bit(L.alive_m, i) && L.health[i] <= 0) died |= 1u << i;
+    }
+    if (died) {
+        int total = 0;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i)
+            if (bit(died, i)) total += L.inv_n[i];
+        // angles = 2*pi*rng.random(total), popped from the end per dying body
+        // (dead bodies in id order, items in slot order)
+        double ang[C::AM * C::SM];
+#pragma unroll
+        for (int k = 0; k < C::AM * C::SM; ++k) {
+            ang[k] = 0.0;
+            if (k < total) ang[k] = 6.283185307179586 * pcg_random(L);
+        }
+        int top = total;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            if (!bit(died, i)) continue;
+#pragma unroll
+            for (int k = 0; k < C::SM; ++k) {
+                if (k >= L.inv_n[i]) continue;
+                --top;
+                float a = (float)sel(ang, top);
+                V2 off = from_polar(P.dd_r, a);
+                V2 p = add(L.c[i], off);
+                int meta = L.inv_meta[i][k];
+                if (it_kind(meta) == kItemHeal) spawn_heal(L, p);
+                else spawn_bitem(L, p, L.inv_hx[i][k], L.inv_hy[i][k],
+                                 mk_bimeta(it_rot(meta), it_copied(meta), it_owner(meta)));
+            }
+            L.inv_n[i] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            if (!bit(died, i)) continue;
+            kill_cause[i] = L.cause[i];
+            L.alive_m &= ~(1u << i);
+            L.awake_m &= ~(1u << i);
+            L.as_touch[i] = 0;
+#pragma unroll
+            for (int s = 0; s < C::NS; ++s) { L.as_ni[i][s] = 0.0f; L.as_ti[i][s] = 0.0f; }
+#pragma unroll
+            for (int j = 0; j < C::AM; ++j) {
+                if (j == i) continue;
+                int p = j < i ? aa_index<C::AM>(j, i) : aa_index<C::AM>(i, j);
+                L.aa_touch &= ~(1u << p);
+                L.aa_ni[p] = 0.0f;
+                L.aa_ti[p] = 0.0f;
+            }
+        }
+    }
+    // AutoPickup.post_step (semantics.py:278-283): every agent's list first
+    {
+        uint32_t lb[C::AM], lh[C::AM];
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            lb[i] = 0;
+            lh[i] = 0;
+            if (!bit(L.alive_m, i)) continue;
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b)
+                if (b < L.nbi && circle_test_point(P.pickup_r, L.c[i], L.ip[b])) lb[i] |= 1u << b;
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h)
+                if (h < L.nheal && circle_test_point(P.pickup_r, L.c[i], L.hp[h])) lh[i] |= 1u << h;
+        }
+        uint32_t takenb = 0, takenh = 0;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b) {
+                if (!bit(lb[i], b)) continue;
+                int im = L.imeta[b];
+                if (inv_take(L, P, i, mk_itmeta(kItemBox, bi_rot(im), bi_copied(im), bi_owner(im)), L.ihx[b], L.ihy[b]))
+                    takenb |= 1u << b;
+            }
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h) {
+                if (!bit(lh[i], h)) continue;
+                if (inv_take(L, P, i, mk_itmeta(kItemHeal, 0, 0, kCauseNone), 0.0f, 0.0f)) takenh |= 1u << h;
+            }
+        }
+        if (takenb) {
+            int wi = 0;
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b) {
+                if (b >= L.nbi || bit(takenb, b)) continue;
+                V2 p = L.ip[b];
+                float hx = L.ihx[b], hy = L.ihy[b];
+                int m = L.imeta[b];
+                uint32_t sb = scr.sn(BIdx<C>::bitem + b);
+#pragma unroll
+                for (int k = 0; k < C::BM; ++k)
+                    if (k == wi && k <= b) { L.ip[k] = p; L.ihx[k] = hx; L.ihy[k] = hy; L.imeta[k] = m; }
+                scr.sn(BIdx<C>::bitem + wi) = sb;
+                ++wi;
+            }
+            L.nbi = wi;
+        }
+        if (takenh) {
+            int wi = 0;
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h) {
+                if (h >= L.nheal || bit(takenh, h)) continue;
+                V2 p = L.hp[h];
+                uint32_t sb = scr.sn(BIdx<C>::heal + h);
+#pragma unroll
+                for (int k = 0; k < C::HM; ++k)
+                    if (k == wi && k <= h) L.hp[k] = p;
+                scr.sn(BIdx<C>::heal + wi) = sb;
+                ++wi;
+            }
+            L.nheal = wi;
+        }
+    }
+    // SafeZone.post_step (semantics.py:758-768): damage outliers, then tick
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!bit(L.alive_m, i)) continue;
+        if (L.endgame || !circle_test_point(L.zrad, L.zpos, L.c[i])) agent_damage(L, P, i, -P.zone_damage, kCauseZone);
+    }
+    zone_tick(L, P);
+    // ---------------- compute_rewards (masurvival_env.py:757-803) ----------------
+    float r[C::AM];
+    int last_kills[C::AM];
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) { r[i] = 0.0f; last_kills[i] = 0; }
+    if (!P.teams) {
+        int first_dead = -1;
+#pragma unroll
+        for (int i = C::AM - 1; i >= 0; --i)
+            if (i < A && !bit(L.alive_m, i)) first_dead = i;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) r[i] += bit(L.alive_m, i) ? P.r_alive : P.r_dead;
+#pragma unroll
+        for (int k = 0; k < C::AM; ++k) {
+            if (!bit(died, k)) continue;
+            int c = kill_cause[k];
+            int idx = -1;
+            if (c >= 0 && c < C::AM && bit(L.alive_m, c)) idx = c;
+            else if (c == kCauseNone && first_dead >= 0) idx = first_dead;  // None in indexed_agents
+#pragma unroll
+            for (int i = 0; i < C::AM; ++i)
+                if (i == idx) { r[i] += P.r_kill; last_kills[i] += 1; }
+        }
+#pragma unroll
+        for (int k = 0; k < C::AM; ++k)
+            if (bit(died, k)) r[k] += P.r_death;
+    } else {
+        bool talive[2] = {false, false};
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i)
+            if (i < A && bit(L.alive_m, i)) talive[team_of(P, i)] = true;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < C::AM; ++i)
+                if (i < A && team_of(P, i) == t) r[i] += talive[t] ? P.r_alive : P.r_dead;
+#pragma unroll
+        for (int k = 0; k < C::AM; ++k) {
+            if (!bit(died, k)) continue;
+            int c = kill_cause[k];
+            if (c != kCauseBadge && c != kCauseBadge + 1) continue;
+            int t = c - kCauseBadge;
+#pragma unroll
+            for (int i = 0; i < C::AM; ++i)
+                if (i < A && team_of(P, i) == t) r[i] += P.r_kill;
+            last_kills[t] += 1;
+        }
+#pragma unroll
+        for (int k = 0; k < C::AM; ++k) {
+            if (!bit(died, k)) continue;
+            int t = team_of(P, k);
+#pragma unroll
+            for (int i = 0; i < C::AM; ++i)
+                if (i < A && team_of(P, i) == t) r[i] += P.r_death;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) rew[i] = r[i];
+    // ---------------- is_done (masurvival_env.py:810-831) ----------------
+    int n_alive = 0;
+    if (P.teams) {
+        bool t0 = false, t1 = false;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            if (i >= A || !bit(L.alive_m, i)) continue;
+            if (team_of(P, i) == 0) t0 = true;
+            else t1 = true;
+        }
+        n_alive = (t0 ? 1 : 0) + (t1 ? 1 : 0);
+    } else {
+        n_alive = __popc(L.alive_m);
+    }
+    bool done = P.gameover == 1 ? (n_alive <= 1) : (n_alive == 0);
+    // ---------------- _update_stats (masurvival_env.py:483-508) ----------------
+    const int R = P.teams ? 2 : A;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (q >= R) continue;
+        int j = P.teams ? (q == 0 ? 0 : A / 2) : q;
+        L.stats[q] += sel(r, j);
+        L.stats[8 + q] += (float)last_kills[q];
+    }
+    L.stats[16] += 1.0f;
+    L.stats[17] += (float)uses_heal;
+    L.stats[18] += (float)uses_box;
+    return done;
+}
+
+}  // namespace mas

@@ -1,0 +1,158 @@
+"""VecMaSurvival: N MaSurvival envs stepped by the HIP kernels (libmas.so).
+
+The batched surface of the build: ``reset() -> obs[N,A,D]``,
+``step(actions int[N,A,6]) -> (obs[N,A,D], rewards[N,A], done[N], info)``,
+all torch tensors resident on the GPU.  Each env is one reference
+``MaSurvival`` (masurvival_env.py:241-389) with its own numpy PCG64 stream;
+``step`` auto-resets finished envs (the returned obs rows are then the first
+observation of the new episode, rewards/done describe the finished step).
+There is no CPU fallback: construction fails loudly without the HIP library
+or a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+from typing import Any, Dict, Optional, Sequence
+
+import numpy as np
+
+from . import spaces
+from .abi import MAS_STATS_WIDTH, MasObsLayout, check, load_library
+from .config import ResolvedConfig, pcg64_state
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class VecMaSurvival:
+    def __init__(self, config: Optional[Dict[str, Dict[str, Any]]] = None, n_envs: int = 1, device=None,
+                 seeds: Optional[Sequence[int]] = None, auto_reset: bool = True):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError('VecMaSurvival needs a ROCm GPU (the env step runs only as HIP kernels)')
+        self.rc = ResolvedConfig(config)
+        self.n_envs = int(n_envs)
+        self.device = torch.device('cuda', torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        self.auto_reset = bool(auto_reset)
+        self._lib = load_library()
+        self._cfg = self.rc.to_struct()
+        h = ctypes.c_void_p()
+        check(self._lib.mas_create(ctypes.byref(self._cfg), self.n_envs, self.device.index, ctypes.byref(h)))
+        self._h = h
+        lay = MasObsLayout()
+        check(self._lib.mas_get_obs_layout(self._h, ctypes.byref(lay)))
+        self.n_agents = lay.n_agents
+        self.obs_dim = lay.obs_dim
+        self.layout = OrderedDict()
+        for k in range(lay.n_keys):
+            name = lay.key_name[k].value.decode()
+            nd = lay.key_ndim[k]
+            shape = (lay.key_shape[k][0],) if nd == 1 else (lay.key_shape[k][0], lay.key_shape[k][1])
+            self.layout[name] = (lay.key_offset[k], shape)
+        N, A, D = self.n_envs, self.n_agents, self.obs_dim
+        dev = self.device
+        self.obs = torch.zeros((N, A, D), dtype=torch.float32, device=dev)
+        self.rewards = torch.zeros((N, A), dtype=torch.float32, device=dev)
+        self.dones = torch.zeros((N,), dtype=torch.uint8, device=dev)
+        self._act = torch.zeros((N, A, 6), dtype=torch.int8, device=dev)
+        self.observation_space = self._single_obs_space()
+        self.action_space = spaces.Tuple((spaces.MultiDiscrete([3, 3, 3, 2, 2, 2]),) * A)
+        self.seed(seeds)
+
+    # ------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
+
+    def _single_obs_space(self):
+        R = dict(low=float('-inf'), high=float('inf'))
+        d = {k: spaces.Box(**R, shape=(self.n_agents,) + shp) for k, (_, shp) in self.layout.items()}
+        return spaces.Dict(d)
+
+    def seed(self, seeds: Optional[Sequence[int]] = None):
+        """One numpy ``default_rng(seed)`` stream per env (env e: seeds[e], default e)."""
+        if seeds is None:
+            seeds = range(self.n_envs)
+        seeds = list(seeds)
+        if len(seeds) != self.n_envs:
+            raise ValueError('need one seed per env')
+        st = np.stack([pcg64_state(int(s)) for s in seeds]).astype(np.uint64)
+        self.set_rng_states(st)
+
+    def set_rng_states(self, states: np.ndarray):
+        """Inject raw numpy PCG64 states, uint64 [N, 6] (see config.pcg64_state)."""
+        st = np.ascontiguousarray(states, dtype=np.uint64)
+        assert st.shape == (self.n_envs, 6)
+        _torch().cuda.synchronize(self.device)
+        check(self._lib.mas_seed(self._h, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), self._stream()))
+
+    def reset(self, mask=None):
+        """BaseEnv.reset for every env (or those with mask != 0); returns obs [N,A,D]."""
+        mptr = None
+        if mask is not None:
+            mask = mask.to(device=self.device, dtype=torch_uint8()).contiguous()
+            mptr = ctypes.c_void_p(mask.data_ptr())
+        check(self._lib.mas_reset(self._h, mptr, ctypes.c_void_p(self.obs.data_ptr()), self._stream()))
+        return self.obs
+
+    def step(self, actions, out=None):
+        """actions: int tensor [N,A,6] (MultiDiscrete [3,3,3,2,2,2]).
+        out: optional (obs, rewards, done) tensors to write into (e.g. a
+        rollout-buffer slice); defaults to the env's own buffers."""
+        torch = _torch()
+        a = actions
+        if a.dtype != torch.int8 or a.device != self.device or not a.is_contiguous():
+            self._act.copy_(a)
+            a = self._act
+        obs, rew, done = (self.obs, self.rewards, self.dones) if out is None else out
+        check(self._lib.mas_step(self._h, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(obs.data_ptr()),
+                                 ctypes.c_void_p(rew.data_ptr()), ctypes.c_void_p(done.data_ptr()),
+                                 int(self.auto_reset), self._stream()))
+        return obs, rew, done, {}
+
+    def flush_stats(self):
+        """Per-env stats accumulated since the last flush, float [N, 19]
+        (reward0..7, kills0..7, steps, heals_used, boxes_placed)."""
+        torch = _torch()
+        s = torch.zeros((self.n_envs, MAS_STATS_WIDTH), dtype=torch.float32, device=self.device)
+        check(self._lib.mas_flush_stats(self._h, ctypes.c_void_p(s.data_ptr()), self._stream()))
+        return s
+
+    def split(self, flat):
+        """View a [..., A, D] obs tensor as the reference's obs dict."""
+        out = OrderedDict()
+        for k, (off, shp) in self.layout.items():
+            size = int(np.prod(shp))
+            out[k] = flat[..., off:off + size].reshape(*flat.shape[:-1], *shp)
+        return out
+
+    def state_bytes(self) -> int:
+        return int(self._lib.mas_state_bytes(self._h))
+
+    def get_state(self):
+        torch = _torch()
+        buf = torch.empty((self.state_bytes(),), dtype=torch.uint8, device=self.device)
+        check(self._lib.mas_get_state(self._h, ctypes.c_void_p(buf.data_ptr()), self._stream()))
+        return buf
+
+    def set_state(self, buf):
+        assert buf.numel() == self.state_bytes() and buf.device == self.device
+        check(self._lib.mas_set_state(self._h, ctypes.c_void_p(buf.data_ptr()), self._stream()))
+
+    def close(self):
+        if getattr(self, '_h', None) is not None and self._h.value:
+            self._lib.mas_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def torch_uint8():
+    return _torch().uint8

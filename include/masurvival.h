@@ -126,8 +126,9 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards,
 
 /* Per-env episode statistics (flush_stats, masurvival_env.py:471-508):
  * device float [n_envs][MAS_STATS_WIDTH] laid out as
- * reward0..reward{R-1}, kills0..kills{R-1}, steps, heals_used, boxes_placed
- * with R = 2 (teams) or n_agents.  Accumulated since the last flush. */
+ * [0,8) reward0..reward{R-1}, [8,16) kills0..kills{R-1}, 16 steps,
+ * 17 heals_used, 18 boxes_placed, with R = 2 (teams) or n_agents (unused
+ * slots 0).  Accumulated since the last flush. */
 #define MAS_STATS_WIDTH 19
 int mas_flush_stats(mas_handle* h, float* stats, void* stream);
 

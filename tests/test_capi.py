@@ -1,0 +1,44 @@
+"""The HIP library loads here (no GPU needed to dlopen) and exports every
+symbol include/masurvival.h declares, with the ABI version the header states."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from masurvival import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, 'include', 'masurvival.h')).read()
+    return sorted(set(re.findall(r'^\s*(?:int|int64_t|int32_t|const char\*)\s+(mas_\w+)\s*\(', txt, re.M)))
+
+
+def test_header_symbols_known():
+    syms = header_symbols()
+    assert len(syms) >= 12
+    assert set(syms) == set(abi.SIGNATURES), set(syms) ^ set(abi.SIGNATURES)
+
+
+def test_library_exports_all_symbols():
+    if not os.path.exists(abi.LIB_PATH):
+        import __graft_entry__  # noqa
+        __graft_entry__.build()
+    lib = ctypes.CDLL(abi.LIB_PATH)
+    for s in header_symbols():
+        assert hasattr(lib, s), s
+    lib.mas_abi_version.restype = ctypes.c_int32
+    assert lib.mas_abi_version() == 1
+
+
+def test_create_rejects_bad_config_without_gpu():
+    lib = abi.load_library()
+    from masurvival.config import ResolvedConfig
+    cfg = ResolvedConfig(None).to_struct()
+    cfg.n_agents = 1
+    h = ctypes.c_void_p()
+    rc = lib.mas_create(ctypes.byref(cfg), 4, 0, ctypes.byref(h))
+    assert rc == -1
+    assert b'n_agents' in lib.mas_last_error()

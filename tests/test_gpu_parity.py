@@ -1,0 +1,72 @@
+"""HIP path == C oracle, bit for bit, on the same seeds and actions.
+
+Parity bar: every observation float, reward and done flag identical
+(np.array_equal) -- the kernels restate the oracle's float op order with
+-ffp-contract=off, so the fp32 tolerance is 0.  Cases: every golden episode
+replayed through VecMaSurvival (n_envs=1), and batched seeded episodes with
+auto-reset compared env-by-env against oracle instances."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+import golden_replay as gr  # noqa: E402
+from masurvival import abi  # noqa: E402
+from masurvival.config import C3_CONFIG, ResolvedConfig, pcg64_state  # noqa: E402
+from masurvival.vec_env import VecMaSurvival  # noqa: E402
+from oracle import OracleEnv  # noqa: E402
+
+
+def make_vec(cfg, n, seeds, auto_reset):
+    try:
+        return VecMaSurvival(cfg, n_envs=n, seeds=seeds, auto_reset=auto_reset)
+    except abi.MasError as e:
+        if 'no compiled capacity class' in str(e):
+            pytest.skip(str(e))
+        raise
+
+
+@pytest.mark.parametrize('name', gr.golden_files())
+def test_golden_episode_on_gpu(name):
+    d, cfg = gr.load(name)
+    env = make_vec(cfg, 1, [int(d['env_seed'])], False)
+    obs = env.reset().cpu().numpy()[0]
+    assert np.array_equal(obs, d['obs'][0]), gr.diff(obs, d['obs'][0])
+    acts = torch.as_tensor(d['actions'], device=env.device)
+    for t in range(len(d['done'])):
+        o, r, dn, _ = env.step(acts[t:t + 1])
+        o = o.cpu().numpy()[0]
+        assert np.array_equal(o, d['obs'][t + 1]), (t, gr.diff(o, d['obs'][t + 1]))
+        assert np.array_equal(r.cpu().numpy()[0], d['rewards'][t]), t
+        assert bool(dn.cpu().numpy()[0]) == bool(d['done'][t]), t
+    stats = env.flush_stats().cpu().numpy()[0]
+    bad, ora_stats = gr.replay(name)
+    assert bad is None
+    assert np.array_equal(stats, ora_stats), (stats, ora_stats)
+
+
+@pytest.mark.parametrize('cfg,n,T', [(None, 64, 400), (C3_CONFIG, 128, 300)])
+def test_batched_autoreset_matches_oracle(cfg, n, T):
+    rc = ResolvedConfig(cfg)
+    seeds = list(range(1000, 1000 + n))
+    env = make_vec(cfg, n, seeds, True)
+    ors = [OracleEnv(rc.to_struct(), pcg64_state(s)) for s in seeds]
+    obs = env.reset().cpu().numpy()
+    for e in range(n):
+        assert np.array_equal(obs[e], ors[e].reset()), e
+    rng = np.random.default_rng(7)
+    resets = 0
+    for t in range(T):
+        a = rng.integers(0, [3, 3, 3, 2, 2, 2], size=(n, rc.n_agents, 6)).astype(np.int8)
+        o, r, dn, _ = env.step(torch.as_tensor(a, device=env.device))
+        o, r, dn = o.cpu().numpy(), r.cpu().numpy(), dn.cpu().numpy()
+        for e in range(n):
+            oo, rr, dd = ors[e].step(a[e])
+            if dd:
+                oo = ors[e].reset()
+                resets += 1
+            assert bool(dn[e]) == dd, (t, e)
+            assert np.array_equal(r[e], rr), (t, e)
+            assert np.array_equal(o[e], oo), (t, e, gr.diff(o[e], oo))
+    assert T < 400 or resets > 0
