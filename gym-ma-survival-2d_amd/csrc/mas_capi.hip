@@ -137,6 +137,74 @@ Poly4 poly_set4(const V2* in)
     return P;
 }
 
+
+// ---------------------------------------------------------------------------
+// Rollout-side: GAE(gamma, lambda) over an on-device rollout buffer
+// (not in the reference).  One thread per agent column m
+// (= env*A + agent), walking t = T-1..0; every load/store is coalesced across
+// the wavefront ([t][m] rows).  Rows are prefetched kGaeChunk steps ahead so
+// the dependent recurrence does not wait on HBM latency each step.  The fp64
+// partial sums (sum adv, sum adv^2) feed the advantage normalisation that the
+// trainer all-reduces across ranks.
+constexpr int kGaeChunk = 8;
+
+__global__ __launch_bounds__(256) void k_gae(int T, int64_t M, int A, const float* __restrict__ rew,
+                                             const float* __restrict__ val, const uint8_t* __restrict__ done,
+                                             float gamma, float lam, float* __restrict__ adv,
+                                             float* __restrict__ ret, double* __restrict__ sums)
+{
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t E = M / A;
+    double s1 = 0.0, s2 = 0.0;
+    if (m < M) {
+        const int64_t e = m / A;
+        float a = 0.0f;
+        float vnext = val[(int64_t)T * M + m];
+        int t = T - 1;
+        for (; t >= kGaeChunk - 1; t -= kGaeChunk) {
+            float r[kGaeChunk], v[kGaeChunk], nt[kGaeChunk];
+#pragma unroll
+            for (int k = 0; k < kGaeChunk; ++k) {
+                const int64_t row = t - k;
+                r[k] = rew[row * M + m];
+                v[k] = val[row * M + m];
+                nt[k] = done[row * E + e] ? 0.0f : 1.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < kGaeChunk; ++k) {
+                const float delta = r[k] + gamma * vnext * nt[k] - v[k];
+                a = delta + gamma * lam * nt[k] * a;
+                const int64_t row = t - k;
+                adv[row * M + m] = a;
+                ret[row * M + m] = a + v[k];
+                s1 += (double)a;
+                s2 += (double)a * (double)a;
+                vnext = v[k];
+            }
+        }
+        for (; t >= 0; --t) {
+            const float r = rew[(int64_t)t * M + m], v = val[(int64_t)t * M + m];
+            const float nt = done[(int64_t)t * E + e] ? 0.0f : 1.0f;
+            const float delta = r + gamma * vnext * nt - v;
+            a = delta + gamma * lam * nt * a;
+            adv[(int64_t)t * M + m] = a;
+            ret[(int64_t)t * M + m] = a + v;
+            s1 += (double)a;
+            s2 += (double)a * (double)a;
+            vnext = v;
+        }
+    }
+    // wavefront (64) butterfly, then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        s1 += __shfl_xor(s1, off, 64);
+        s2 += __shfl_xor(s2, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&sums[0], s1);
+        atomicAdd(&sums[1], s2);
+    }
+}
+
 }  // namespace
 
 struct Ops {
@@ -424,6 +492,23 @@ int mas_set_state(mas_handle* h, const void* src, void* stream)
 {
     if (!h || !src) return fail(MAS_ERR_INVALID_ARG, "mas_set_state: null argument");
     HIP_TRY(hipMemcpyAsync(h->state, src, (size_t)mas_state_bytes(h), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return MAS_OK;
+}
+
+int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards, const float* values,
+            const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
+            void* stream)
+{
+    if (T <= 0 || n_columns <= 0 || n_agents <= 0 || n_columns % n_agents)
+        return fail(MAS_ERR_INVALID_ARG, "mas_gae: need T > 0 and n_columns a positive multiple of n_agents");
+    if (!rewards || !values || !done || !advantages || !returns || !adv_sums)
+        return fail(MAS_ERR_INVALID_ARG, "mas_gae: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(adv_sums, 0, 2 * sizeof(double), s));
+    dim3 g((unsigned)((n_columns + 255) / 256));
+    hipLaunchKernelGGL(k_gae, g, dim3(256), 0, s, (int)T, (int64_t)n_columns, (int)n_agents, rewards, values, done,
+                       gamma, lam, advantages, returns, adv_sums);
+    HIP_TRY(hipGetLastError());
     return MAS_OK;
 }
 

@@ -58,6 +58,8 @@ SIGNATURES = {
     'mas_state_bytes': (c_int64, [c_void_p]),
     'mas_get_state': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'mas_set_state': (c_int32, [c_void_p, c_void_p, c_void_p]),
+    'mas_gae': (c_int32, [c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
+                          c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_last_error': (c_char_p, []),
     'mas_abi_version': (c_int32, []),
 }

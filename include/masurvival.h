@@ -138,6 +138,20 @@ int64_t mas_state_bytes(const mas_handle* h);
 int mas_get_state(mas_handle* h, void* dst, void* stream);
 int mas_set_state(mas_handle* h, const void* src, void* stream);
 
+/* Rollout side (SURVEY.md 8(a) a24 -- new, the reference has no trainer):
+ * GAE(gamma, lambda) over an on-device rollout buffer of T steps and
+ * n_columns = n_envs * n_agents agent columns, all DEVICE pointers:
+ *   rewards [T][n_columns], values [T+1][n_columns] (row T = bootstrap value
+ *   of the observation after the last step), done [T][n_envs] (mas_step's
+ *   done; an auto-reset env's next value is masked out),
+ *   advantages/returns [T][n_columns] (out), adv_sums double[2] (out:
+ *   sum and sum of squares of the advantages, for normalisation).
+ *   delta_t = r_t + gamma * V_{t+1} * (1 - d_t) - V_t
+ *   A_t     = delta_t + gamma * lambda * (1 - d_t) * A_{t+1}      */
+int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards, const float* values,
+            const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
+            void* stream);
+
 const char* mas_last_error(void);
 int32_t mas_abi_version(void);
 
