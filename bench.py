@@ -1,9 +1,13 @@
 """Headline benchmark: agent-env-steps/sec for the 2v2 config.
 
-A "step" is one batched MaSurvival.step of every env on this rank (the HIP
-k_step kernel: actions -> 2 Box2D steps -> rules -> obs/rewards/done, with
-auto-reset), inputs resident in HBM.  Actions come from a device RNG
-(random policy) drawn before the timed kernel on the same stream.
+A "step" is one rollout step of every env on this rank, all in HBM: the
+shared policy MLP's forward on the current observations (bf16 autocast),
+Gumbel-max sampling of the six action heads, the batched MaSurvival.step (the
+HIP k_step kernel: actions -> 2 Box2D steps -> rules -> obs/rewards/done with
+auto-reset, writing straight into the rollout buffer), and -- every
+--horizon steps -- the GAE scan (HIP mas_gae) plus one PPO update (1 epoch,
+4 minibatches, gradient all-reduce across ranks).  --mode env times the env
+kernel alone under a device-RNG random policy.
 
 Run: python bench.py [--gpus N --steps K --warmup W --config 2v2 --envs N_per_gpu]
 For N>1 the driver launches one rank per GPU with torch.distributed.run; envs
@@ -63,10 +67,13 @@ def cpu_baseline(cfg, budget_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=200)
-    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=128, help='timed rollout steps (multiple of --horizon amortises the update)')
+    ap.add_argument('--warmup', type=int, default=64)
     ap.add_argument('--config', default='2v2')
     ap.add_argument('--envs', type=int, default=None, help='envs per GPU (default 65536 for 2v2)')
+    ap.add_argument('--mode', choices=['ppo', 'env'], default='ppo',
+                    help='ppo: policy forward + env step + buffer, GAE + PPO update every horizon; env: random actions')
+    ap.add_argument('--horizon', type=int, default=64)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -84,36 +91,67 @@ def main():
     env = VecMaSurvival(cfg, n_envs=n, seeds=range(rank * n, rank * n + n), auto_reset=True)
     A, D = env.n_agents, env.obs_dim
     dev = env.device
-    env.reset()
-    hi = torch.tensor([3, 3, 3, 2, 2, 2], device=dev, dtype=torch.int32)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
-    acts = torch.empty((n, A, 6), dtype=torch.int8, device=dev)
+    # the env kernel's launch duration, HIP events on the stream it runs on
+    kev = []
 
-    def draw():
-        u = torch.rand((n, A, 6), generator=gen, device=dev)
-        acts.copy_((u * hi).to(torch.int8))
+    if args.mode == 'ppo':
+        from masurvival.ppo import PPOConfig, PPOTrainer
+        pcfg = PPOConfig(horizon=args.horizon)
+        tr = PPOTrainer(env, pcfg, seed=0)
+        env_step = env.step
+
+        def timed_env_step(a, out=None):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = env_step(a, out=out)
+            e1.record()
+            kev.append((e0, e1))
+            return r
+        env.step = timed_env_step
+        state = {'t': 0, 'updates': 0}
+
+        def one_step():
+            tr.rollout_step(state['t'])
+            state['t'] += 1
+            if state['t'] == pcfg.horizon:
+                tr.finish_rollout()
+                tr.update()
+                state['t'] = 0
+                state['updates'] += 1
+    else:
+        env.reset()
+        hi = torch.tensor([3, 3, 3, 2, 2, 2], device=dev, dtype=torch.int32)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1234 + rank)
+        acts = torch.empty((n, A, 6), dtype=torch.int8, device=dev)
+
+        def one_step():
+            u = torch.rand((n, A, 6), generator=gen, device=dev)
+            acts.copy_((u * hi).to(torch.int8))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            env.step(acts)
+            e1.record()
+            kev.append((e0, e1))
 
     for _ in range(args.warmup):
-        draw()
-        env.step(acts)
+        one_step()
     torch.cuda.synchronize()
+    kev.clear()
+    if args.mode == 'ppo':
+        state['updates'] = 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        draw()
-        ev[k][0].record()
-        env.step(acts)
-        ev[k][1].record()
+    for _ in range(args.steps):
+        one_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     if world > 1:
         t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -122,6 +160,9 @@ def main():
     total_agent_steps = world * n * A * args.steps
     b_env = algorithmic_bytes_per_env_step(A, env.rc.n_heals, env.rc.n_boxes, D)
     achieved = b_env * n / (kern_ms * 1e-3) / 1e9
+    workload = (f'{args.config} PPO rollout (policy MLP 2x256 bf16 fwd + sample + env step + buffer), '
+                f'GAE + PPO update (1 epoch, 4 minibatches) every {args.horizon} steps'
+                if args.mode == 'ppo' else f'{args.config} env step, random policy')
     line = {
         'metric': 'agent-env-steps/sec (whole node), %s N_envs=%d' % (args.config, n * world),
         'value': total_agent_steps / dt,
@@ -129,12 +170,15 @@ def main():
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt * 1e3 / args.steps,
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'f32', 'data': 'synthetic (device-RNG random policy)',
-        'config': {'workload': f'{args.config} env step, N_envs={n}/GPU, auto-reset, random policy',
-                   'n_envs_per_gpu': n, 'n_agents': A, 'obs_dim': D, 'parallelism': f'env-shard x{world}'},
+        'dtype': 'f32', 'data': 'synthetic (seeded envs, on-device policy sampling)',
+        'config': {'workload': workload, 'n_envs_per_gpu': n, 'n_agents': A, 'obs_dim': D,
+                   'horizon': args.horizon if args.mode == 'ppo' else None,
+                   'updates_in_timed_region': state['updates'] if args.mode == 'ppo' else 0,
+                   'parallelism': f'env-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                     'kernel': 'k_step', 'kernel_ms': kern_ms, 'bytes_per_env_step': b_env},
+                     'kernel': 'k_step (mas_step)', 'kernel_ms': kern_ms, 'bytes_per_env_step': b_env,
+                     'bytes_per_launch': b_env * n},
         'cpu_baseline': None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -67,11 +67,11 @@ __global__ void k_seed(uint32_t* __restrict__ state, int64_t N, const uint64_t* 
     // st_hi, st_lo, inc_hi, inc_lo as (lo, hi) word pairs, then has32, u32
     for (int k = 0; k < 4; ++k) {
         uint64_t x = st6[e * 6 + k];
-        state[(int64_t)(w_rng + 2 * k) * N + e] = (uint32_t)(x & 0xffffffffULL);
-        state[(int64_t)(w_rng + 2 * k + 1) * N + e] = (uint32_t)(x >> 32);
+        state[state_index(w_rng + 2 * k, e, N)] = (uint32_t)(x & 0xffffffffULL);
+        state[state_index(w_rng + 2 * k + 1, e, N)] = (uint32_t)(x >> 32);
     }
-    state[(int64_t)w_has32 * N + e] = (uint32_t)st6[e * 6 + 4];
-    state[(int64_t)(w_has32 + 1) * N + e] = (uint32_t)st6[e * 6 + 5];
+    state[state_index(w_has32, e, N)] = (uint32_t)st6[e * 6 + 4];
+    state[state_index(w_has32 + 1, e, N)] = (uint32_t)st6[e * 6 + 5];
 }
 
 __global__ void k_stats(uint32_t* __restrict__ state, int64_t N, int w_stats, float* __restrict__ out)
@@ -79,11 +79,11 @@ __global__ void k_stats(uint32_t* __restrict__ state, int64_t N, int w_stats, fl
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= N) return;
     for (int k = 0; k < kStats; ++k) {
-        uint32_t u = state[(int64_t)(w_stats + k) * N + e];
+        uint32_t u = state[state_index(w_stats + k, e, N)];
         float f;
         __builtin_memcpy(&f, &u, 4);
         out[e * kStats + k] = f;
-        state[(int64_t)(w_stats + k) * N + e] = 0u;
+        state[state_index(w_stats + k, e, N)] = 0u;
     }
 }
 
@@ -352,6 +352,16 @@ static int build_params(mas_handle* h)
         P.wall_angle[2] = 0.0f;
         P.wall_angle[3] = (float)(3.14159265358979323846 / 2.0);
         for (int k = 0; k < kNumWalls; ++k) P.wall_q[k] = rot_of(P.wall_angle[k]);
+        for (int k = 0; k < kNumWalls; ++k) {
+            V2 lo = mk(3.4e38f, 3.4e38f), hi = mk(-3.4e38f, -3.4e38f);
+            for (int v = 0; v < 4; ++v) {
+                V2 w = xmul(P.wall_pos[k], P.wall_q[k], P.wall_poly.v[v]);
+                lo = mk(w.x < lo.x ? w.x : lo.x, w.y < lo.y ? w.y : lo.y);
+                hi = mk(w.x > hi.x ? w.x : hi.x, w.y > hi.y ? w.y : hi.y);
+            }
+            P.wall_lo[k] = lo;
+            P.wall_hi[k] = hi;
+        }
     }
     // Cameras vision cone (simulation.py:321-328)
     {
@@ -411,6 +421,11 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMalloc(&h->state, (size_t)h->ops.info.words * (size_t)n_envs * 4);
     if (e == hipSuccess) e = hipMemset(h->state, 0, (size_t)h->ops.info.words * (size_t)n_envs * 4);
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
+    h->P.prof = nullptr;
+#ifdef MAS_PROFILE
+    if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(h->P.prof, 0, 64 * sizeof(unsigned long long));
+#endif
     if (e != hipSuccess) {
         std::string msg = std::string("mas_create: ") + hipGetErrorString(e);
         if (h->state) hipFree(h->state);
@@ -426,9 +441,23 @@ int mas_destroy(mas_handle* h)
     if (!h) return MAS_OK;
     if (h->state) hipFree(h->state);
     if (h->seedbuf) hipFree(h->seedbuf);
+    if (h->P.prof) hipFree(h->P.prof);
     delete h;
     return MAS_OK;
 }
+
+#ifdef MAS_PROFILE
+// profiling build only (not part of the ABI): copy out and clear the per-phase
+// wave-time accumulators (units: 10 ns ticks of the 100 MHz constant clock).
+int mas_prof_read(mas_handle* h, unsigned long long* host64)
+{
+    if (!h || !host64 || !h->P.prof) return fail(MAS_ERR_INVALID_ARG, "mas_prof_read: not a profiling build");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(host64, h->P.prof, 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(h->P.prof, 0, 64 * sizeof(unsigned long long)));
+    return MAS_OK;
+}
+#endif
 
 int mas_get_obs_layout(const mas_handle* h, mas_obs_layout* out)
 {

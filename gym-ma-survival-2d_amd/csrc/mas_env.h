@@ -69,9 +69,30 @@ struct Params {
     float wall_angle[kNumWalls];
     Rot wall_q[kNumWalls];
     Poly4 cone;
+    V2 wall_lo[kNumWalls], wall_hi[kNumWalls];  // world AABBs of the walls (ray-cast culling)
     // observation key offsets (sorted-key layout); -1 when absent
     int o_agent, o_bi, o_bim, o_bs, o_bsm, o_box, o_boxm, o_hs, o_hsm, o_heal, o_healm, o_oth, o_othm, o_zone;
+    unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
+
+// Phase timing for the profiling build (make prof -> libmas_prof.so): lane 0
+// of each wave adds the constant-clock (100 MHz) time since the previous mark
+// to P.prof[k].  Marks sit only at wave-convergent points of k_step.
+#ifdef MAS_PROFILE
+__device__ __forceinline__ void prof_mark(const Params& P, int k)
+{
+    __shared__ unsigned long long t_last;
+    unsigned long long t = wall_clock64();
+    if (threadIdx.x == 0) {
+        if (k >= 0) atomicAdd(&P.prof[k], t - t_last);
+        t_last = t;
+    }
+}
+#define MAS_PROF(P, k) ::mas::prof_mark(P, k)
+#else
+#define MAS_PROF(P, k) ((void)0)
+#endif
+enum ProfPhase { kPfLoad, kPfCollide, kPfSolve, kPfToi, kPfStore, kPfCount };
 
 // ---------------------------------------------------------------------------
 // select helpers for runtime indices into register arrays
@@ -115,6 +136,11 @@ MAS_HD void put2(T (&a)[N][M], int i, int j, T v)
 // ---------------------------------------------------------------------------
 // env state in registers
 // ---------------------------------------------------------------------------
+template <class C>
+constexpr int kSeenWords = (C::NB + 3) / 4;
+
+MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (((int64_t)(w >> 2)) * N + e) * 4 + (w & 3); }
+
 template <class C>
 struct EnvL {
     // agents (slot = IndexBodies id)
@@ -160,32 +186,81 @@ struct EnvL {
     uint64_t st_hi, st_lo, inc_hi, inc_lo;
     uint32_t has32, u32v;
     float stats[kStats];
+    // Cameras.seen as bytes: byte k of the packed words = bitmask over camera
+    // positions (rank among alive agents) that see body k (BIdx order)
+    uint32_t seenw[kSeenWords<C>];
 };
 
-// visit every persistent word (load / store / count), fixed order
+// State groups: each phase kernel loads the groups it reads and stores the
+// groups it writes (kernels in mas_kernels.inc), so a kernel's register
+// footprint is its working set, not the whole env.
+enum : uint32_t {
+    kGDyn = 1u << 0,    // agent pose / velocity / sleep, alive & awake masks
+    kGRule = 1u << 1,   // health, cause, cooldown, inventories
+    kGBox = 1u << 2,    // boxes group
+    kGItem = 1u << 3,   // box_items group
+    kGPend = 1u << 4,   // Object.next_spawns
+    kGHeal = 1u << 5,   // heals group
+    kGZone = 1u << 6,   // SafeZone
+    kGCont = 1u << 7,   // contact memory
+    kGRng = 1u << 8,    // PCG64 stream
+    kGStat = 1u << 9,   // flush_stats accumulators
+    kGSeen = 1u << 10,  // camera seen-by bytes (Cameras.seen, consumed by the obs kernel)
+    kGAll = (1u << 11) - 1,
+};
+
+// visit every persistent word in a fixed order; f.on gates the groups not in
+// `mask` (the word cursor still advances, so offsets never depend on it).
+// Groups start on 4-word boundaries: HBM image is AoSoA, word w of env e at
+// state[((w / 4) * N + e) * 4 + w % 4], so a lane moves 4 words with one
+// 16-B access and a wave's access is 1 KiB contiguous (state_index below).
 template <class C, class F>
-MAS_HD void visit_state(EnvL<C>& L, F& f)
+MAS_HD void visit_state(EnvL<C>& L, F& f, uint32_t mask = kGAll)
 {
+    f.on = (mask & kGDyn) != 0;
 #pragma unroll
     for (int i = 0; i < C::AM; ++i) {
         f.io(L.c[i].x); f.io(L.c[i].y); f.io(L.a[i]); f.io(L.v[i].x); f.io(L.v[i].y); f.io(L.w[i]);
-        f.io(L.sleep[i]); f.io(L.health[i]); f.io(L.cause[i]); f.io(L.cooldown[i]); f.io(L.inv_n[i]);
+        f.io(L.sleep[i]);
+    }
+    f.io(L.alive_m); f.io(L.awake_m);
+    f.align4();
+    f.on = (mask & kGRule) != 0;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        f.io(L.health[i]); f.io(L.cause[i]); f.io(L.cooldown[i]); f.io(L.inv_n[i]);
 #pragma unroll
         for (int k = 0; k < C::SM; ++k) { f.io(L.inv_meta[i][k]); f.io(L.inv_hx[i][k]); f.io(L.inv_hy[i][k]); }
     }
-    f.io(L.alive_m); f.io(L.awake_m);
-    f.io(L.nbox); f.io(L.nbi); f.io(L.npend); f.io(L.nheal);
+    f.align4();
+    f.on = (mask & kGBox) != 0;
+    f.io(L.nbox);
 #pragma unroll
     for (int b = 0; b < C::BM; ++b) {
         f.io(L.bp[b].x); f.io(L.bp[b].y); f.io(L.bhx[b]); f.io(L.bhy[b]); f.io(L.bmeta[b]); f.io(L.bhealth[b]);
-        f.io(L.ip[b].x); f.io(L.ip[b].y); f.io(L.ihx[b]); f.io(L.ihy[b]); f.io(L.imeta[b]);
-        f.io(L.pp[b].x); f.io(L.pp[b].y); f.io(L.phx[b]); f.io(L.phy[b]); f.io(L.pmeta[b]);
     }
+    f.align4();
+    f.on = (mask & kGItem) != 0;
+    f.io(L.nbi);
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) { f.io(L.ip[b].x); f.io(L.ip[b].y); f.io(L.ihx[b]); f.io(L.ihy[b]); f.io(L.imeta[b]); }
+    f.align4();
+    f.on = (mask & kGPend) != 0;
+    f.io(L.npend);
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) { f.io(L.pp[b].x); f.io(L.pp[b].y); f.io(L.phx[b]); f.io(L.phy[b]); f.io(L.pmeta[b]); }
+    f.align4();
+    f.on = (mask & kGHeal) != 0;
+    f.io(L.nheal);
 #pragma unroll
     for (int h = 0; h < C::HM; ++h) { f.io(L.hp[h].x); f.io(L.hp[h].y); }
+    f.align4();
+    f.on = (mask & kGZone) != 0;
 #pragma unroll
     for (int k = 0; k < kMaxPhases; ++k) { f.io(L.zc[k].x); f.io(L.zc[k].y); }
     f.io(L.phase); f.io(L.t_cd); f.io(L.t_sh); f.io(L.endgame); f.io(L.zpos.x); f.io(L.zpos.y); f.io(L.zrad);
+    f.align4();
+    f.on = (mask & kGCont) != 0;
     f.io(L.aa_touch);
 #pragma unroll
     for (int p = 0; p < (C::NAA > 0 ? C::NAA : 1); ++p) { f.io(L.aa_ni[p]); f.io(L.aa_ti[p]); }
@@ -196,14 +271,25 @@ MAS_HD void visit_state(EnvL<C>& L, F& f)
         for (int s = 0; s < C::NS; ++s) { f.io(L.as_ni[i][s]); f.io(L.as_ti[i][s]); }
     }
     f.io(L.inv_dt0);
+    f.align4();
+    f.on = (mask & kGRng) != 0;
     f.io64(L.st_hi); f.io64(L.st_lo); f.io64(L.inc_hi); f.io64(L.inc_lo);
     f.io(L.has32); f.io(L.u32v);
+    f.align4();
+    f.on = (mask & kGStat) != 0;
 #pragma unroll
     for (int k = 0; k < kStats; ++k) f.io(L.stats[k]);
+    f.align4();
+    f.on = (mask & kGSeen) != 0;
+#pragma unroll
+    for (int k = 0; k < kSeenWords<C>; ++k) f.io(L.seenw[k]);
+    f.align4();
 }
 
 struct WordCounter {
     int n = 0;
+    bool on = true;
+    MAS_HD void align4() { n = (n + 3) & ~3; }
     template <class T> MAS_HD void io(T&) { n += 1; }
     template <class T> MAS_HD void io64(T&) { n += 2; }
 };

@@ -1232,11 +1232,14 @@ __device__ __forceinline__ void world_step(EnvL<C>& L, const Params& P, float dt
             update_as_g(L, P, i, s, g, ln, lp);
         }
     }
+    MAS_PROF(P, kPfCollide);
     world_solve(L, P, S, dt, dtRatio);
+    MAS_PROF(P, kPfSolve);
     for (int i = 0; i < C::AM; ++i) {  // runtime loop: toi_agent indexes agents via sel/put
         if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
         toi_agent(L, P, S, i, dt);
     }
+    MAS_PROF(P, kPfToi);
     L.inv_dt0 = inv_dt;
 }
 

@@ -15,11 +15,12 @@ constexpr int kWG = 64;  // threads (= envs) per workgroup: one wave
 // per-thread LDS scratch
 template <class C>
 struct Scr {
-    uint32_t* cand;   // [C::NB][kWG] camera candidates
+    uint16_t* pairs;  // [C::AM * C::NB][kWG] (camera, agent, candidate body) of update_seen
     uint32_t* seen;   // [C::NB][kWG] seen-by camera-position bitmask per body
     uint8_t* perm;    // [256][kWG] spawn-grid permutation
     int tid;
-    __device__ uint32_t& cd(int k) { return cand[k * kWG + tid]; }
+    static constexpr int kPairs = C::AM * C::NB;
+    __device__ uint16_t& pr(int k) { return pairs[k * kWG + tid]; }
     __device__ uint32_t& sn(int k) { return seen[k * kWG + tid]; }
     __device__ uint8_t& pm(int k) { return perm[k * kWG + tid]; }
 };
@@ -97,47 +98,206 @@ __device__ __forceinline__ int ray_cast(const EnvL<C>& L, const Params& P, V2 p1
     return hit;
 }
 
+// Fixture table: per-lane LDS copy of what a ray test needs by runtime body
+// index (positions of every body, box half-extents + meta), [field][kWG]
+// interleaved so a wave's 64 lanes hit 64 distinct banks.
+template <class C>
+struct FixTab {
+    float* f;  // [2*NB + 3*BM][kWG]
+    int tid;
+    static constexpr int kWords = 2 * C::NB + 3 * C::BM;
+    __device__ float& px(int k) const { return f[k * kWG + tid]; }
+    __device__ float& py(int k) const { return f[(C::NB + k) * kWG + tid]; }
+    __device__ float& hx(int b) const { return f[(2 * C::NB + b) * kWG + tid]; }
+    __device__ float& hy(int b) const { return f[(2 * C::NB + C::BM + b) * kWG + tid]; }
+    __device__ float& meta(int b) const { return f[(2 * C::NB + 2 * C::BM + b) * kWG + tid]; }
+};
+
+template <class C>
+__device__ __forceinline__ void build_fixtab(const EnvL<C>& L, const Params& P, const FixTab<C>& T)
+{
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        T.px(BIdx<C>::box + b) = L.bp[b].x;
+        T.py(BIdx<C>::box + b) = L.bp[b].y;
+        T.hx(b) = L.bhx[b];
+        T.hy(b) = L.bhy[b];
+        T.meta(b) = __int_as_float(L.bmeta[b]);
+        T.px(BIdx<C>::bitem + b) = L.ip[b].x;
+        T.py(BIdx<C>::bitem + b) = L.ip[b].y;
+    }
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h) {
+        T.px(BIdx<C>::heal + h) = L.hp[h].x;
+        T.py(BIdx<C>::heal + h) = L.hp[h].y;
+    }
+#pragma unroll
+    for (int w = 0; w < kNumWalls; ++w) {
+        T.px(BIdx<C>::wall + w) = P.wall_pos[w].x;
+        T.py(BIdx<C>::wall + w) = P.wall_pos[w].y;
+    }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        T.px(BIdx<C>::agent + i) = L.c[i].x;
+        T.py(BIdx<C>::agent + i) = L.c[i].y;
+    }
+}
+
+// ray_cast with Box2D's own broadphase test in front: b2DynamicTree::RayCast
+// only reports fixtures whose AABB the segment overlaps (segment AABB +
+// separating axis).  The cull runs for every body with static indices; the
+// exact b2Shape::RayCast then runs only over the surviving bodies, in
+// canonical order, by runtime index from the fixture table.  A culled body
+// cannot intersect the segment, so its exact test would have rejected it for
+// any max fraction: the result is identical to ray_cast (the margin absorbs
+// rounding).  Loop trips = the lane's survivors, not all NB bodies.
+template <class C>
+__device__ __forceinline__ int ray_cast_tab(const EnvL<C>& L, const Params& P, const FixTab<C>& T, V2 p1, V2 p2)
+{
+    constexpr float m = 1e-3f;
+    const V2 r = sub(p2, p1);
+    const float rl = len(r);
+    const V2 rn = rl > 0.0f ? scl(1.0f / rl, r) : mk(0.0f, 0.0f);
+    const V2 v = mk(-rn.y, rn.x);
+    const V2 av = mk(fabsf(v.x), fabsf(v.y));
+    const float lox = fminf(p1.x, p2.x) - m, loy = fminf(p1.y, p2.y) - m;
+    const float hix = fmaxf(p1.x, p2.x) + m, hiy = fmaxf(p1.y, p2.y) + m;
+    auto keep = [&](V2 c, float ex, float ey) -> bool {
+        if (c.x - ex > hix || c.x + ex < lox || c.y - ey > hiy || c.y + ey < loy) return false;
+        return fabsf(dot(v, sub(p1, c))) - (av.x * ex + av.y * ey) <= m;
+    };
+    uint64_t mask = 0;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (b < L.nbox && keep(L.bp[b], L.bhx[b], L.bhy[b])) mask |= 1ull << (BIdx<C>::box + b);
+        if (b < L.nbi && keep(L.ip[b], P.bitem_r, P.bitem_r)) mask |= 1ull << (BIdx<C>::bitem + b);
+    }
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h)
+        if (h < L.nheal && keep(L.hp[h], P.heal_r, P.heal_r)) mask |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+    for (int w = 0; w < kNumWalls; ++w) {
+        V2 c = scl(0.5f, add(P.wall_lo[w], P.wall_hi[w]));
+        V2 e = scl(0.5f, sub(P.wall_hi[w], P.wall_lo[w]));
+        if (keep(c, e.x + m, e.y + m)) mask |= 1ull << (BIdx<C>::wall + w);
+    }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+        if (bit(L.alive_m, i) && keep(L.c[i], P.agent_r, P.agent_r)) mask |= 1ull << (BIdx<C>::agent + i);
+
+    float maxf = 1.0f;
+    int hit = -1;
+    while (mask) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const V2 c = mk(T.px(k), T.py(k));
+        float f;
+        const bool is_box = k < BIdx<C>::bitem;
+        const bool is_wall = k >= BIdx<C>::wall && k < BIdx<C>::agent;
+        if (is_box || is_wall) {
+            Poly4 poly;
+            Rot q = kIdRot;
+            V2 pos = c;
+            if (is_box) {
+                const int meta = __float_as_int(T.meta(k));
+                poly = box_poly(T.hx(k), T.hy(k), box_rot(meta), box_copied(meta));
+            } else {
+                poly = P.wall_poly;
+                const int w = k - BIdx<C>::wall;
+#pragma unroll
+                for (int q2 = 0; q2 < kNumWalls; ++q2)
+                    if (q2 == w) { q.s = opq(P.wall_q[q2].s); q.c = opq(P.wall_q[q2].c); }
+            }
+            f = ray_poly(poly, pos, q, p1, p2, maxf);
+        } else {
+            const float rad = k < BIdx<C>::heal ? P.bitem_r : (k < BIdx<C>::wall ? P.heal_r : P.agent_r);
+            f = ray_circle(rad, c, p1, p2, maxf);
+        }
+        if (f >= 0.0f) {
+            hit = k;
+            maxf = f;
+            if (maxf == 0.0f) break;
+        }
+    }
+    return hit;
+}
+
 // Cameras._update_seen (simulation.py:336-354): camera list position p =
 // rank among the alive agents; scr.sn(body) gets bit p when body is in the
-// vision cone and the LOS ray to pos + (1+1e-6)*d hits it first.
+// vision cone and the LOS ray to pos + (1+1e-6)*d hits it first.  All
+// (camera, candidate) pairs of the env go into one list so a wave iterates
+// max(pairs per env), not sum over cameras of max(candidates per camera).
 template <class C>
-__device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, Scr<C>& scr)
+__device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, Scr<C>& scr, const FixTab<C>& T)
 {
 #pragma unroll
     for (int k = 0; k < C::NB; ++k) scr.sn(k) = 0u;
-    int p = 0;
+    int p = 0, np = 0;
+#pragma unroll
     for (int i = 0; i < C::AM; ++i) {
         if (!bit(L.alive_m, i)) continue;
-        V2 pos = sel(L.c, i);
-        Rot q = rot_of(sel(L.a, i));
-        int nc = 0;
+        const V2 pos = L.c[i];
+        const Rot q = rot_of(L.a[i]);
+        const uint32_t tag = ((uint32_t)p << 11) | ((uint32_t)i << 8);
 #pragma unroll
         for (int b = 0; b < C::BM; ++b)
-            if (b < L.nbox && poly_test_point(P.cone, pos, q, L.bp[b])) scr.cd(nc++) = BIdx<C>::box + b;
+            if (b < L.nbox && poly_test_point(P.cone, pos, q, L.bp[b])) scr.pr(np++) = tag | (BIdx<C>::box + b);
 #pragma unroll
         for (int b = 0; b < C::BM; ++b)
-            if (b < L.nbi && poly_test_point(P.cone, pos, q, L.ip[b])) scr.cd(nc++) = BIdx<C>::bitem + b;
+            if (b < L.nbi && poly_test_point(P.cone, pos, q, L.ip[b])) scr.pr(np++) = tag | (BIdx<C>::bitem + b);
 #pragma unroll
         for (int h = 0; h < C::HM; ++h)
-            if (h < L.nheal && poly_test_point(P.cone, pos, q, L.hp[h])) scr.cd(nc++) = BIdx<C>::heal + h;
+            if (h < L.nheal && poly_test_point(P.cone, pos, q, L.hp[h])) scr.pr(np++) = tag | (BIdx<C>::heal + h);
 #pragma unroll
         for (int w = 0; w < kNumWalls; ++w)
-            if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) scr.cd(nc++) = BIdx<C>::wall + w;
+            if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) scr.pr(np++) = tag | (BIdx<C>::wall + w);
 #pragma unroll
         for (int j = 0; j < C::AM; ++j)
             if (j != i && bit(L.alive_m, j) && poly_test_point(P.cone, pos, q, L.c[j]))
-                scr.cd(nc++) = BIdx<C>::agent + j;
-        const float eps1 = (float)(1.0 + 1e-6);
-        for (int k = 0; k < nc; ++k) {
-            int body = (int)scr.cd(k);
-            V2 oc = body_pos(L, P, body);
-            V2 d = sub(oc, pos);
-            V2 end = add(pos, scl(eps1, d));
-            int hit = ray_cast(L, P, pos, end);
-            if (hit == body) scr.sn(body) |= 1u << p;
-        }
+                scr.pr(np++) = tag | (BIdx<C>::agent + j);
         ++p;
     }
+    const float eps1 = (float)(1.0 + 1e-6);
+    for (int t = 0; t < np; ++t) {
+        const uint32_t e = scr.pr(t);
+        const int body = (int)(e & 0xffu), i = (int)((e >> 8) & 7u), cam = (int)(e >> 11);
+        const V2 pos = mk(T.px(BIdx<C>::agent + i), T.py(BIdx<C>::agent + i));
+        const V2 oc = mk(T.px(body), T.py(body));
+        const V2 d = sub(oc, pos);
+        const V2 end = add(pos, scl(eps1, d));
+        if (ray_cast_tab(L, P, T, pos, end) == body) scr.sn(body) |= 1u << cam;
+    }
+}
+
+// Cameras.seen <-> state bytes (kGSeen): byte k = camera-position mask of body k
+template <class C>
+__device__ __forceinline__ void seen_pack(EnvL<C>& L, Scr<C>& scr)
+{
+#pragma unroll
+    for (int w = 0; w < kSeenWords<C>; ++w) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * w + q < C::NB) x |= (scr.sn(4 * w + q) & 0xffu) << (8 * q);
+        L.seenw[w] = x;
+    }
+}
+
+template <class C>
+__device__ __forceinline__ uint32_t seen_of(const EnvL<C>& L, int k)  // k static
+{
+    return (L.seenw[k >> 2] >> (8 * (k & 3))) & 0xffu;
+}
+
+// byte k (runtime) := v
+template <class C>
+__device__ __forceinline__ void seen_put(EnvL<C>& L, int k, uint32_t v)
+{
+#pragma unroll
+    for (int w = 0; w < kSeenWords<C>; ++w)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * w + q == k) L.seenw[w] = (L.seenw[w] & ~(0xffu << (8 * q))) | ((v & 0xffu) << (8 * q));
 }
 
 // Health._change_health for agents (semantics.py:490-500); teammates are
@@ -217,12 +377,8 @@ __device__ __forceinline__ void spawn_box(EnvL<C>& L, const Params& P, V2 pos, f
         L.bhy[b] = hy;
         L.bmeta[b] = mk_boxmeta(rot, copied, 0, vuln, kCauseNone);
         L.bhealth[b] = 0;
-#pragma unroll
-        for (int i = 0; i < C::AM; ++i) {
-            L.as_touch[i] &= ~(1u << (kNumWalls + b));
-            L.as_ni[i][kNumWalls + b] = 0.0f;
-            L.as_ti[i][kNumWalls + b] = 0.0f;
-        }
+        // contact memory of static slot b is already zero: slots >= nbox are
+        // cleared by the despawn compaction and by reset (invariant)
     }
     L.nbox = nb + 1;
 }
@@ -257,10 +413,10 @@ __device__ __forceinline__ void spawn_heal(EnvL<C>& L, V2 pos)
 // ---------------------------------------------------------------------------
 // observation row writer: fetch_observations (masurvival_env.py:510-657)
 // ---------------------------------------------------------------------------
-template <class C>
-__device__ __forceinline__ void write_obs(const EnvL<C>& L, const Params& P, Scr<C>& scr, float* __restrict__ obs_env)
+template <class C, class Sink>
+__device__ __forceinline__ void write_obs_row(const EnvL<C>& L, const Params& P, int i, Sink& row)
 {
-    const int A = P.A, D = P.D, as_ = P.as_;
+    const int A = P.A, as_ = P.as_;
     int post_pos[C::AM];
     int np = 0;
 #pragma unroll
@@ -283,55 +439,53 @@ __device__ __forceinline__ void write_obs(const EnvL<C>& L, const Params& P, Scr
         for (int k = 0; k < kMaxPhases; ++k)
             if (k == ph) zone6[5] = opq(P.zradf[k]);
     }
-#pragma unroll
-    for (int i = 0; i < C::AM; ++i) {
-        if (i >= A) continue;
-        float* row = obs_env + (size_t)i * D;
+    {
         bool alive = bit(L.alive_m, i);
-        int pp = post_pos[i];
+        int pp = sel(post_pos, i);
         // agent + others rows (_fetch_agents_observations :659-704)
+        // (sections outside the sink's column window are skipped: uniform test)
+        const bool w_agents = row.want(P.o_agent, as_) || row.want(P.o_oth, (A - 1) * as_) ||
+                              row.want(P.o_othm, A - 1);
 #pragma unroll
         for (int j = 0; j < C::AM; ++j) {
+            if (!w_agents) continue;
             if (j >= A) continue;
-            float r[9];
-            int k = 0;
-            r[k++] = (float)j;
-            if (P.teams) r[k++] = (float)team_of(P, j);
             bool aj = bit(L.alive_m, j);
-            r[k++] = aj ? (float)L.health[j] : 0.0f;
-            r[k++] = aj ? L.c[j].x : 0.0f;
-            r[k++] = aj ? L.c[j].y : 0.0f;
-            r[k++] = aj ? L.a[j] : 0.0f;
-            r[k++] = aj ? L.v[j].x : 0.0f;
-            r[k++] = aj ? L.v[j].y : 0.0f;
-            r[k++] = aj ? L.w[j] : 0.0f;
-            int base;
-            if (j == i) base = P.o_agent;
-            else base = P.o_oth + (j < i ? j : j - 1) * as_;
-            for (int q = 0; q < as_; ++q) row[base + q] = r[q];
+            int o = j == i ? P.o_agent : P.o_oth + (j < i ? j : j - 1) * as_;
+            row(o++, (float)j);
+            if (P.teams) row(o++, (float)team_of(P, j));
+            row(o++, aj ? (float)L.health[j] : 0.0f);
+            row(o++, aj ? L.c[j].x : 0.0f);
+            row(o++, aj ? L.c[j].y : 0.0f);
+            row(o++, aj ? L.a[j] : 0.0f);
+            row(o++, aj ? L.v[j].x : 0.0f);
+            row(o++, aj ? L.v[j].y : 0.0f);
+            row(o++, aj ? L.w[j] : 0.0f);
             if (j != i) {
                 // others_mask: seen list at the post-despawn list index (quirk D1)
                 float m = 1.0f;
-                if (alive && aj && (scr.sn(BIdx<C>::agent + j) >> pp) & 1u) m = 0.0f;
-                row[P.o_othm + (j < i ? j : j - 1)] = m;
+                if (alive && aj && (seen_of(L, BIdx<C>::agent + j) >> pp) & 1u) m = 0.0f;
+                row(P.o_othm + (j < i ? j : j - 1), m);
             }
         }
+        if (row.want(P.o_zone, 6)) {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) row[P.o_zone + q] = zone6[q];
-        if (P.H > 0) {
+            for (int q = 0; q < 6; ++q) row(P.o_zone + q, zone6[q]);
+        }
+        if (P.H > 0 && (row.want(P.o_heal, 2 * P.H) || row.want(P.o_healm, P.H))) {
 #pragma unroll
             for (int h = 0; h < C::HM; ++h) {
                 if (h >= P.H) continue;
                 bool present = h < L.nheal;
-                row[P.o_heal + 2 * h] = present ? L.hp[h].x : 0.0f;
-                row[P.o_heal + 2 * h + 1] = present ? L.hp[h].y : 0.0f;
+                row(P.o_heal + 2 * h, present ? L.hp[h].x : 0.0f);
+                row(P.o_heal + 2 * h + 1, present ? L.hp[h].y : 0.0f);
                 float m;
                 if (P.omniscient) m = present ? 0.0f : 1.0f;
-                else m = (present && alive && ((scr.sn(BIdx<C>::heal + h) >> pp) & 1u)) ? 0.0f : 1.0f;
-                row[P.o_healm + h] = m;
+                else m = (present && alive && ((seen_of(L, BIdx<C>::heal + h) >> pp) & 1u)) ? 0.0f : 1.0f;
+                row(P.o_healm + h, m);
             }
         }
-        if (P.B > 0) {
+        if (P.B > 0 && (row.want(P.o_box, 11 * P.B) || row.want(P.o_boxm, P.B))) {
 #pragma unroll
             for (int b = 0; b < C::BM; ++b) {
                 if (b >= P.B) continue;
@@ -339,17 +493,19 @@ __device__ __forceinline__ void write_obs(const EnvL<C>& L, const Params& P, Scr
                 Poly4 poly = box_poly(L.bhx[b], L.bhy[b], box_rot(L.bmeta[b]), box_copied(L.bmeta[b]));
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
-                    row[P.o_box + 11 * b + 2 * v] = present ? poly.v[v].x : 0.0f;
-                    row[P.o_box + 11 * b + 2 * v + 1] = present ? poly.v[v].y : 0.0f;
+                    row(P.o_box + 11 * b + 2 * v, present ? poly.v[v].x : 0.0f);
+                    row(P.o_box + 11 * b + 2 * v + 1, present ? poly.v[v].y : 0.0f);
                 }
-                row[P.o_box + 11 * b + 8] = present ? L.bp[b].x : 0.0f;
-                row[P.o_box + 11 * b + 9] = present ? L.bp[b].y : 0.0f;
-                row[P.o_box + 11 * b + 10] = 0.0f;  // box bodies always have angle 0
+                row(P.o_box + 11 * b + 8, present ? L.bp[b].x : 0.0f);
+                row(P.o_box + 11 * b + 9, present ? L.bp[b].y : 0.0f);
+                row(P.o_box + 11 * b + 10, 0.0f);  // box bodies always have angle 0
                 float m;
                 if (P.omniscient) m = present ? 0.0f : 1.0f;
-                else m = (present && alive && ((scr.sn(BIdx<C>::box + b) >> pp) & 1u)) ? 0.0f : 1.0f;
-                row[P.o_boxm + b] = m;
+                else m = (present && alive && ((seen_of(L, BIdx<C>::box + b) >> pp) & 1u)) ? 0.0f : 1.0f;
+                row(P.o_boxm + b, m);
             }
+        }
+        if (P.B > 0 && (row.want(P.o_bi, 10 * P.B) || row.want(P.o_bim, P.B))) {
 #pragma unroll
             for (int b = 0; b < C::BM; ++b) {
                 if (b >= P.B) continue;
@@ -357,40 +513,42 @@ __device__ __forceinline__ void write_obs(const EnvL<C>& L, const Params& P, Scr
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     V2 cv = box_corner(L.ihx[b], L.ihy[b], bi_rot(L.imeta[b]) + v);
-                    row[P.o_bi + 10 * b + 2 * v] = present ? cv.x : 0.0f;
-                    row[P.o_bi + 10 * b + 2 * v + 1] = present ? cv.y : 0.0f;
+                    row(P.o_bi + 10 * b + 2 * v, present ? cv.x : 0.0f);
+                    row(P.o_bi + 10 * b + 2 * v + 1, present ? cv.y : 0.0f);
                 }
-                row[P.o_bi + 10 * b + 8] = present ? L.ip[b].x : 0.0f;
-                row[P.o_bi + 10 * b + 9] = present ? L.ip[b].y : 0.0f;
+                row(P.o_bi + 10 * b + 8, present ? L.ip[b].x : 0.0f);
+                row(P.o_bi + 10 * b + 9, present ? L.ip[b].y : 0.0f);
                 float m;
                 if (P.omniscient) m = present ? 0.0f : 1.0f;
-                else m = (present && alive && ((scr.sn(BIdx<C>::bitem + b) >> pp) & 1u)) ? 0.0f : 1.0f;
-                row[P.o_bim + b] = m;
+                else m = (present && alive && ((seen_of(L, BIdx<C>::bitem + b) >> pp) & 1u)) ? 0.0f : 1.0f;
+                row(P.o_bim + b, m);
             }
         }
         // usable inventory slots (:620-654)
         int lastmeta = 0;
         float lhx = 0.0f, lhy = 0.0f;
-        if (alive && L.inv_n[i] > 0) {
-            int n = L.inv_n[i] - 1;
-            lastmeta = sel(L.inv_meta[i], n);
-            lhx = sel(L.inv_hx[i], n);
-            lhy = sel(L.inv_hy[i], n);
+        const int ninv = sel(L.inv_n, i);
+        const bool w_slots = row.want(P.o_hs, 1) || row.want(P.o_hsm, 1) || row.want(P.o_bs, 8) ||
+                             row.want(P.o_bsm, 1);
+        if (w_slots && alive && ninv > 0) {
+            lastmeta = sel2(L.inv_meta, i, ninv - 1);
+            lhx = sel2(L.inv_hx, i, ninv - 1);
+            lhy = sel2(L.inv_hy, i, ninv - 1);
         }
-        if (P.H > 0) {
+        if (w_slots && P.H > 0) {
             bool isheal = it_kind(lastmeta) == kItemHeal;
-            row[P.o_hs] = isheal ? (float)P.healing : 0.0f;
-            row[P.o_hsm] = isheal ? 0.0f : 1.0f;
+            row(P.o_hs, isheal ? (float)P.healing : 0.0f);
+            row(P.o_hsm, isheal ? 0.0f : 1.0f);
         }
-        if (P.B > 0) {
+        if (w_slots && P.B > 0) {
             bool isbox = it_kind(lastmeta) == kItemBox;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 V2 cv = box_corner(lhx, lhy, it_rot(lastmeta) + v);
-                row[P.o_bs + 2 * v] = isbox ? cv.x : 0.0f;
-                row[P.o_bs + 2 * v + 1] = isbox ? cv.y : 0.0f;
+                row(P.o_bs + 2 * v, isbox ? cv.x : 0.0f);
+                row(P.o_bs + 2 * v + 1, isbox ? cv.y : 0.0f);
             }
-            row[P.o_bsm] = isbox ? 0.0f : 1.0f;
+            row(P.o_bsm, isbox ? 0.0f : 1.0f);
         }
     }
 }
@@ -561,10 +719,14 @@ __device__ __forceinline__ void zone_tick(EnvL<C>& L, const Params& P)
 }
 
 // ---------------------------------------------------------------------------
-// one env step: BaseEnv.step (masurvival_env.py:76-90)
+// one env step: BaseEnv.step (masurvival_env.py:76-90), in three phases that
+// run as separate kernels (mas_kernels.inc): step_pre (queue_actions + the
+// pre_step hooks), step_phys (2 x world.Step + boxes Health.post_step), then
+// Cameras (update_seen) and step_post (the rest of post_step, rewards, done).
 // ---------------------------------------------------------------------------
 template <class C>
-__device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& scr, const int8_t* __restrict__ act, float* rew)
+__device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixTab<C>& T,
+                                         const int8_t* __restrict__ act)
 {
     const int A = P.A;
     // queue_actions (masurvival_env.py:741-755): alive agents only
@@ -661,12 +823,13 @@ __device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& sc
     // Melee / ContinuousMelee (semantics.py:531-554, 584-610): all rays first
     {
         int target[C::AM];
+        build_fixtab(L, P, T);
         for (int i = 0; i < C::AM; ++i) {
             int tg = -1;
             if (bit(L.alive_m, i)) {
                 V2 c = sel(L.c, i);
                 V2 hand = from_polar(P.melee_range, sel(L.a, i));
-                tg = ray_cast(L, P, c, add(c, hand));
+                tg = ray_cast_tab(L, P, T, c, add(c, hand));
             }
             put(target, i, tg);
         }
@@ -688,10 +851,17 @@ __device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& sc
                 if (L.cooldown[i] > 0) L.cooldown[i] -= 1;
         }
     }
+    L.stats[17] += (float)uses_heal;
+    L.stats[18] += (float)uses_box;
+}
+
+template <class C>
+__device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P)
+{
     // ---------------- physics: 2 x world.Step(1/60, 10, 10) ----------------
     const float dt = (float)(1.0 / 60.0);
-    world_step(L, P, dt);
-    world_step(L, P, dt);
+#pragma unroll 1
+    for (int k = 0; k < 2; ++k) world_step(L, P, dt);
     // ---------------- post_step ----------------
     // boxes: Health.post_step + Object / OwnedObject despawn (semantics.py:429-435, 858-861, 907-912)
     {
@@ -753,8 +923,14 @@ __device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& sc
             }
         }
     }
-    // agents: Cameras.post_step over the pre-despawn list
-    update_seen(L, P, scr);
+}
+
+// agents: Cameras.post_step over the pre-despawn list runs between step_phys
+// and step_post (k_cameras); step_post reads and compacts its bytes.
+template <class C>
+__device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, float* rew)
+{
+    const int A = P.A;
     // agents: Health.post_step -> despawn dead (id order): TrackDeaths, IndexBodies,
     // DeathDrop (semantics.py:387-396), Inventory, Health.pre_despawn -> TrackKills
     uint32_t died = 0;
@@ -853,11 +1029,11 @@ __device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& sc
                 V2 p = L.ip[b];
                 float hx = L.ihx[b], hy = L.ihy[b];
                 int m = L.imeta[b];
-                uint32_t sb = scr.sn(BIdx<C>::bitem + b);
+                uint32_t sb = seen_of(L, BIdx<C>::bitem + b);
 #pragma unroll
                 for (int k = 0; k < C::BM; ++k)
                     if (k == wi && k <= b) { L.ip[k] = p; L.ihx[k] = hx; L.ihy[k] = hy; L.imeta[k] = m; }
-                scr.sn(BIdx<C>::bitem + wi) = sb;
+                seen_put(L, BIdx<C>::bitem + wi, sb);
                 ++wi;
             }
             L.nbi = wi;
@@ -868,11 +1044,11 @@ __device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& sc
             for (int h = 0; h < C::HM; ++h) {
                 if (h >= L.nheal || bit(takenh, h)) continue;
                 V2 p = L.hp[h];
-                uint32_t sb = scr.sn(BIdx<C>::heal + h);
+                uint32_t sb = seen_of(L, BIdx<C>::heal + h);
 #pragma unroll
                 for (int k = 0; k < C::HM; ++k)
                     if (k == wi && k <= h) L.hp[k] = p;
-                scr.sn(BIdx<C>::heal + wi) = sb;
+                seen_put(L, BIdx<C>::heal + wi, sb);
                 ++wi;
             }
             L.nheal = wi;
@@ -968,8 +1144,6 @@ __device__ __forceinline__ bool env_step(EnvL<C>& L, const Params& P, Scr<C>& sc
         L.stats[8 + q] += (float)last_kills[q];
     }
     L.stats[16] += 1.0f;
-    L.stats[17] += (float)uses_heal;
-    L.stats[18] += (float)uses_box;
     return done;
 }
 

@@ -1,0 +1,242 @@
+"""On-device PPO rollout for VecMaSurvival.
+
+The reference ships no trainer; this is the consumer the batched env step is
+built for.  Everything stays in HBM:
+
+* ``RolloutBuffer`` -- obs [T+1, N, A, D] (the env kernel writes each step's
+  observation straight into row t+1), actions int8 [T, N, A, 6], log-probs,
+  values [T+1, N, A], rewards [T, N, A], dones uint8 [T, N]; advantages and
+  returns [T, N, A].
+* GAE(gamma, lambda) is the HIP ``mas_gae`` kernel (one lane per agent
+  column, backward over T), which also returns the fp64 advantage sums.
+* The policy is a shared-parameter MLP (obs D -> 256 -> 256, tanh) with six
+  categorical heads (MultiDiscrete [3,3,3,2,2,2]) and a value head; forward
+  passes run under bf16 autocast (hipBLASLt GEMMs), losses in fp32.
+
+Multi-GPU (one process per GPU, envs sharded): the only collectives are one
+fp64 all-reduce of (sum adv, sum adv^2, count) per rollout and one flat
+gradient all-reduce (average) per minibatch -- RCCL over xGMI when the process
+group is 'nccl', gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .abi import check, load_library
+
+HEADS = (3, 3, 3, 2, 2, 2)
+N_LOGITS = sum(HEADS)
+
+
+@dataclass
+class PPOConfig:
+    horizon: int = 64          # T
+    gamma: float = 0.99
+    lam: float = 0.95
+    hidden: int = 256
+    lr: float = 3e-4
+    epochs: int = 1
+    minibatches: int = 4
+    clip: float = 0.2
+    vf_coef: float = 0.5
+    ent_coef: float = 0.01
+    max_grad_norm: float = 0.5
+    autocast_bf16: bool = True
+
+
+class PolicyMLP(nn.Module):
+    """Shared across agents: obs [.., D] -> (logits [.., 15], value [..])."""
+
+    def __init__(self, obs_dim: int, hidden: int = 256):
+        super().__init__()
+        self.body = nn.Sequential(nn.Linear(obs_dim, hidden), nn.Tanh(), nn.Linear(hidden, hidden), nn.Tanh())
+        self.head = nn.Linear(hidden, N_LOGITS + 1)
+
+    def forward(self, x):
+        h = self.head(self.body(x))
+        return h[..., :N_LOGITS].float(), h[..., N_LOGITS].float()
+
+
+def _split_heads(logits):
+    return torch.split(logits, HEADS, dim=-1)
+
+
+def sample_actions(logits, gen: Optional[torch.Generator] = None):
+    """Gumbel-max sample of the six heads; returns (int8 [.., 6], logp [..])."""
+    acts, logp = [], 0.0
+    for lg in _split_heads(logits):
+        lsm = F.log_softmax(lg, dim=-1)
+        u = torch.rand(lg.shape, device=lg.device, generator=gen).clamp_(1e-20, 1.0)
+        a = torch.argmax(lsm - torch.log(-torch.log(u)), dim=-1)
+        acts.append(a)
+        logp = logp + lsm.gather(-1, a.unsqueeze(-1)).squeeze(-1)
+    return torch.stack(acts, dim=-1).to(torch.int8), logp
+
+
+def evaluate_actions(logits, actions):
+    """log-prob and entropy of given actions [.., 6]."""
+    logp, ent = 0.0, 0.0
+    a = actions.long()
+    for k, lg in enumerate(_split_heads(logits)):
+        lsm = F.log_softmax(lg, dim=-1)
+        logp = logp + lsm.gather(-1, a[..., k:k + 1]).squeeze(-1)
+        ent = ent - (lsm.exp() * lsm).sum(-1)
+    return logp, ent
+
+
+def gae(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents, stream=None):
+    """HIP GAE over [T, N*A] columns (include/masurvival.h mas_gae)."""
+    lib = load_library()
+    T = rewards.shape[0]
+    M = rewards[0].numel()
+    for t in (rewards, values, adv_out, ret_out):
+        assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+    assert values.shape[0] == T + 1 and dones.shape[0] == T and dones.dtype == torch.uint8
+    assert dones[0].numel() * n_agents == M and sums_out.dtype == torch.float64
+    s = stream if stream is not None else torch.cuda.current_stream(rewards.device).cuda_stream
+    check(lib.mas_gae(T, M, n_agents, ctypes.c_void_p(rewards.data_ptr()), ctypes.c_void_p(values.data_ptr()),
+                      ctypes.c_void_p(dones.data_ptr()), float(gamma), float(lam),
+                      ctypes.c_void_p(adv_out.data_ptr()), ctypes.c_void_p(ret_out.data_ptr()),
+                      ctypes.c_void_p(sums_out.data_ptr()), ctypes.c_void_p(s)))
+
+
+def gae_reference(rewards, values, dones, gamma, lam, n_agents):
+    """Plain torch fp32 restatement of mas_gae (the numerics test's reference)."""
+    T = rewards.shape[0]
+    r = rewards.reshape(T, -1)
+    v = values.reshape(T + 1, -1)
+    nt = 1.0 - dones.reshape(T, -1).float().repeat_interleave(n_agents, dim=1)
+    adv = torch.zeros_like(r)
+    a = torch.zeros_like(r[0])
+    for t in range(T - 1, -1, -1):
+        delta = r[t] + gamma * v[t + 1] * nt[t] - v[t]
+        a = delta + gamma * lam * nt[t] * a
+        adv[t] = a
+    return adv.reshape(rewards.shape), (adv + v[:T]).reshape(rewards.shape)
+
+
+def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents, stream=None):
+    """Same contract as gae() on host tensors -- test double for the CPU
+    multi-process tests only (the product trainer always runs the HIP kernel)."""
+    adv, ret = gae_reference(rewards, values, dones, gamma, lam, n_agents)
+    adv_out.copy_(adv)
+    ret_out.copy_(ret)
+    sums_out[0] = adv.double().sum()
+    sums_out[1] = (adv.double() ** 2).sum()
+
+
+class RolloutBuffer:
+    def __init__(self, T, N, A, D, device):
+        self.T, self.N, self.A, self.D = T, N, A, D
+        f = dict(device=device, dtype=torch.float32)
+        self.obs = torch.zeros((T + 1, N, A, D), **f)
+        self.actions = torch.zeros((T, N, A, 6), device=device, dtype=torch.int8)
+        self.logp = torch.zeros((T, N, A), **f)
+        self.values = torch.zeros((T + 1, N, A), **f)
+        self.rewards = torch.zeros((T, N, A), **f)
+        self.dones = torch.zeros((T, N), device=device, dtype=torch.uint8)
+        self.adv = torch.zeros((T, N, A), **f)
+        self.ret = torch.zeros((T, N, A), **f)
+        self.adv_sums = torch.zeros((2,), device=device, dtype=torch.float64)
+
+
+def _allreduce_grads(params, world, group=None):
+    """One flat bucket (~0.5 MB for the 2x256 MLP): a single RCCL ring
+    all-reduce per minibatch instead of one per parameter tensor."""
+    grads = [p.grad for p in params]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    flat.div_(world)
+    off = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n
+
+
+class PPOTrainer:
+    """Collect T steps of every env on this rank, GAE on device, PPO update."""
+
+    def __init__(self, env, cfg: PPOConfig = PPOConfig(), seed: int = 0, group=None):
+        self.env, self.cfg = env, cfg
+        self.device = env.device
+        self.group = group
+        self.world = dist.get_world_size(group) if group is not None or dist.is_initialized() else 1
+        torch.manual_seed(seed)  # identical init on every rank
+        self.policy = PolicyMLP(env.obs_dim, cfg.hidden).to(self.device)
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr, eps=1e-5)
+        self.buf = RolloutBuffer(cfg.horizon, env.n_envs, env.n_agents, env.obs_dim, self.device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed * 7919 + (dist.get_rank() if dist.is_initialized() else 0))
+        self.buf.obs[0].copy_(env.reset())
+        self.last_stats = {}
+        self.gae_impl = gae  # the HIP kernel; CPU tests inject gae_reference_into
+
+    def _fwd(self, x):
+        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.cfg.autocast_bf16):
+            return self.policy(x)
+
+    @torch.no_grad()
+    def rollout_step(self, t):
+        b = self.buf
+        logits, v = self._fwd(b.obs[t])
+        a, lp = sample_actions(logits, self.gen)
+        b.actions[t].copy_(a)
+        b.logp[t].copy_(lp)
+        b.values[t].copy_(v)
+        self.env.step(b.actions[t], out=(b.obs[t + 1], b.rewards[t], b.dones[t]))
+
+    @torch.no_grad()
+    def finish_rollout(self):
+        b, c = self.buf, self.cfg
+        _, v = self._fwd(b.obs[c.horizon])
+        b.values[c.horizon].copy_(v)
+        self.gae_impl(b.rewards, b.values, b.dones, c.gamma, c.lam, b.adv, b.ret, b.adv_sums, self.env.n_agents)
+        stats = torch.cat([b.adv_sums, torch.tensor([float(b.adv.numel())], device=self.device,
+                                                     dtype=torch.float64)])
+        if self.world > 1:
+            dist.all_reduce(stats, group=self.group)
+        mean = stats[0] / stats[2]
+        var = (stats[1] / stats[2] - mean * mean).clamp_min(0.0)
+        b.adv.sub_(mean.float()).div_(var.sqrt().float() + 1e-8)
+
+    def update(self):
+        b, c = self.buf, self.cfg
+        M = c.horizon * b.N * b.A
+        obs = b.obs[:c.horizon].reshape(M, b.D)
+        acts = b.actions.reshape(M, 6)
+        old_lp, adv, ret = b.logp.reshape(M), b.adv.reshape(M), b.ret.reshape(M)
+        params = list(self.policy.parameters())
+        mb = M // c.minibatches
+        for _ in range(c.epochs):
+            perm = torch.randperm(M, device=self.device, generator=self.gen)
+            for k in range(c.minibatches):
+                idx = perm[k * mb:(k + 1) * mb]
+                logits, v = self._fwd(obs[idx])
+                lp, ent = evaluate_actions(logits, acts[idx])
+                ratio = torch.exp(lp - old_lp[idx])
+                a = adv[idx]
+                pg = -torch.min(ratio * a, ratio.clamp(1 - c.clip, 1 + c.clip) * a).mean()
+                vl = F.mse_loss(v, ret[idx])
+                loss = pg + c.vf_coef * vl - c.ent_coef * ent.mean()
+                self.opt.zero_grad(set_to_none=False)
+                loss.backward()
+                if self.world > 1:
+                    _allreduce_grads(params, self.world, self.group)
+                nn.utils.clip_grad_norm_(params, c.max_grad_norm)
+                self.opt.step()
+        self.last_stats = {'loss': loss.detach(), 'pg': pg.detach(), 'v': vl.detach()}
+        b.obs[0].copy_(b.obs[c.horizon])
+
+    def iteration(self):
+        for t in range(self.cfg.horizon):
+            self.rollout_step(t)
+        self.finish_rollout()
+        self.update()
