@@ -157,6 +157,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, kern_ms = float(t[0]), float(t[1])
 
+    diag = env.debug_counters()
     total_agent_steps = world * n * A * args.steps
     b_env = algorithmic_bytes_per_env_step(A, env.rc.n_heals, env.rc.n_boxes, D)
     achieved = b_env * n / (kern_ms * 1e-3) / 1e9
@@ -174,7 +175,8 @@ def main():
         'config': {'workload': workload, 'n_envs_per_gpu': n, 'n_agents': A, 'obs_dim': D,
                    'horizon': args.horizon if args.mode == 'ppo' else None,
                    'updates_in_timed_region': state['updates'] if args.mode == 'ppo' else 0,
-                   'parallelism': f'env-shard x{world}'},
+                   'parallelism': f'env-shard x{world}',
+                   'phys_general_envs_last_step': diag['phys_general_envs']},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
                      'kernel': 'k_step (mas_step)', 'kernel_ms': kern_ms, 'bytes_per_env_step': b_env,

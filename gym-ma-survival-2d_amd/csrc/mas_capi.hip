@@ -20,7 +20,7 @@ using namespace mas;
 
 namespace mas {
 struct ClassInfo {
-    int words, w_rng, w_has32, w_stats, lds_bytes;
+    int words, w_rng, w_has32, w_stats, w_cont, lds_bytes;
 };
 #define MAS_DECLARE(NAME)                                                                                     \
     ClassInfo class_info_##NAME();                                                                          \
@@ -221,6 +221,7 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
+    int* phys;  // [N] env list + [1] count (k_phys_fast -> k_phys)
     mas_obs_layout layout;
 };
 
@@ -417,11 +418,17 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
         return fail(MAS_ERR_UNSUPPORTED, "mas_create: no compiled capacity class fits this config (classes: " MAS_CLASS_LIST ")");
     }
     build_params(h);
+    h->P.w_cont = h->ops.info.w_cont;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipMalloc(&h->state, (size_t)h->ops.info.words * (size_t)n_envs * 4);
     if (e == hipSuccess) e = hipMemset(h->state, 0, (size_t)h->ops.info.words * (size_t)n_envs * 4);
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
     h->P.prof = nullptr;
+    h->phys = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 1) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 1) * sizeof(int));
+    h->P.phys_list = h->phys;
+    h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
 #ifdef MAS_PROFILE
     if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(h->P.prof, 0, 64 * sizeof(unsigned long long));
@@ -441,7 +448,8 @@ int mas_destroy(mas_handle* h)
     if (!h) return MAS_OK;
     if (h->state) hipFree(h->state);
     if (h->seedbuf) hipFree(h->seedbuf);
-    if (h->P.prof) hipFree(h->P.prof);
+    if (h->P.prof) (void)hipFree(h->P.prof);
+    if (h->phys) (void)hipFree(h->phys);
     delete h;
     return MAS_OK;
 }
@@ -538,6 +546,16 @@ int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards
     hipLaunchKernelGGL(k_gae, g, dim3(256), 0, s, (int)T, (int64_t)n_columns, (int)n_agents, rewards, values, done,
                        gamma, lam, advantages, returns, adv_sums);
     HIP_TRY(hipGetLastError());
+    return MAS_OK;
+}
+
+int mas_debug_counters(mas_handle* h, int64_t* host_out)
+{
+    if (!h || !host_out) return fail(MAS_ERR_INVALID_ARG, "mas_debug_counters: null argument");
+    int c = 0;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&c, h->P.phys_count, sizeof(int), hipMemcpyDeviceToHost));
+    host_out[0] = c;
     return MAS_OK;
 }
 

@@ -64,6 +64,7 @@ struct Params {
     double floor_size;
     int grid_size;
     float inv_mass, inv_I, lin_damp, ang_damp;
+    int w_cont;  // first state word of the contact memory (kGCont)
     Poly4 wall_poly;
     V2 wall_pos[kNumWalls];
     float wall_angle[kNumWalls];
@@ -72,6 +73,8 @@ struct Params {
     V2 wall_lo[kNumWalls], wall_hi[kNumWalls];  // world AABBs of the walls (ray-cast culling)
     // observation key offsets (sorted-key layout); -1 when absent
     int o_agent, o_bi, o_bim, o_bs, o_bsm, o_box, o_boxm, o_hs, o_hsm, o_heal, o_healm, o_oth, o_othm, o_zone;
+    int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
+    int* phys_count;  // number of them
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
 
@@ -139,7 +142,61 @@ MAS_HD void put2(T (&a)[N][M], int i, int j, T v)
 template <class C>
 constexpr int kSeenWords = (C::NB + 3) / 4;
 
+constexpr int kLanes = 64;  // one wave per workgroup in every env kernel
+
+// Contact memory of one env (b2Contact: touching flag + the manifold point's
+// accumulated normal / tangent impulse) for the agent-agent pairs (i<j,
+// aa_index order) and the agent-static pairs (agent-major, statics = walls
+// then boxes).  Kept in LDS, [word][kLanes], by the kernels that touch it
+// (k_phys, k_post, k_reset): every access is by runtime pair index at LDS
+// cost instead of a select over the whole table in registers.  The HBM image
+// holds the same words in the same order (state group kGCont).
+template <class C>
+struct Cont {
+    static constexpr int kNAA = C::NAA > 0 ? C::NAA : 1;
+    static constexpr int kAAT = 0, kAST = 1, kAANI = 1 + C::AM, kAATI = kAANI + kNAA, kASNI = kAATI + kNAA,
+                         kASTI = kASNI + C::AM * C::NS, kWords = kASTI + C::AM * C::NS;
+    uint32_t* u;
+    int tid;
+    MAS_HD uint32_t& w(int k) const { return u[k * kLanes + tid]; }
+    MAS_HD uint32_t aat() const { return w(kAAT); }
+    MAS_HD void set_aat(uint32_t v) const { w(kAAT) = v; }
+    MAS_HD uint32_t ast(int i) const { return w(kAST + i); }
+    MAS_HD void set_ast(int i, uint32_t v) const { w(kAST + i) = v; }
+    MAS_HD float aani(int p) const { return bits_f(w(kAANI + p)); }
+    MAS_HD float aati(int p) const { return bits_f(w(kAATI + p)); }
+    MAS_HD void set_aani(int p, float v) const { w(kAANI + p) = f_bits(v); }
+    MAS_HD void set_aati(int p, float v) const { w(kAATI + p) = f_bits(v); }
+    MAS_HD float asni(int i, int s) const { return bits_f(w(kASNI + i * C::NS + s)); }
+    MAS_HD float asti(int i, int s) const { return bits_f(w(kASTI + i * C::NS + s)); }
+    MAS_HD void set_asni(int i, int s, float v) const { w(kASNI + i * C::NS + s) = f_bits(v); }
+    MAS_HD void set_asti(int i, int s, float v) const { w(kASTI + i * C::NS + s) = f_bits(v); }
+    MAS_HD void clear() const
+    {
+        for (int k = 0; k < kWords; ++k) w(k) = 0u;
+    }
+    MAS_HD static float bits_f(uint32_t u)
+    {
+        float f;
+        __builtin_memcpy(&f, &u, 4);
+        return f;
+    }
+    MAS_HD static uint32_t f_bits(float f)
+    {
+        uint32_t u;
+        __builtin_memcpy(&u, &f, 4);
+        return u;
+    }
+};
+
+#ifndef MAS_STATE_VEC4
+#define MAS_STATE_VEC4 0
+#endif
+#if MAS_STATE_VEC4
 MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (((int64_t)(w >> 2)) * N + e) * 4 + (w & 3); }
+#else
+MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (int64_t)w * N + e; }
+#endif
 
 template <class C>
 struct EnvL {
@@ -176,11 +233,8 @@ struct EnvL {
     int phase, t_cd, t_sh, endgame;
     V2 zpos;
     float zrad;
-    // contact memory: touching flag + accumulated impulses (b2Manifold points)
-    uint32_t aa_touch;
-    float aa_ni[C::NAA > 0 ? C::NAA : 1], aa_ti[C::NAA > 0 ? C::NAA : 1];
-    uint32_t as_touch[C::AM];
-    float as_ni[C::AM][C::NS], as_ti[C::AM][C::NS];
+    // contact memory (touching flags + accumulated impulses) is not here: it
+    // lives in LDS inside the kernels that use it (Cont below, kGCont)
     float inv_dt0;
     // numpy Generator(PCG64) state
     uint64_t st_hi, st_lo, inc_hi, inc_lo;
@@ -260,17 +314,11 @@ MAS_HD void visit_state(EnvL<C>& L, F& f, uint32_t mask = kGAll)
     for (int k = 0; k < kMaxPhases; ++k) { f.io(L.zc[k].x); f.io(L.zc[k].y); }
     f.io(L.phase); f.io(L.t_cd); f.io(L.t_sh); f.io(L.endgame); f.io(L.zpos.x); f.io(L.zpos.y); f.io(L.zrad);
     f.align4();
-    f.on = (mask & kGCont) != 0;
-    f.io(L.aa_touch);
-#pragma unroll
-    for (int p = 0; p < (C::NAA > 0 ? C::NAA : 1); ++p) { f.io(L.aa_ni[p]); f.io(L.aa_ti[p]); }
-#pragma unroll
-    for (int i = 0; i < C::AM; ++i) {
-        f.io(L.as_touch[i]);
-#pragma unroll
-        for (int s = 0; s < C::NS; ++s) { f.io(L.as_ni[i][s]); f.io(L.as_ti[i][s]); }
-    }
+    f.on = (mask & kGDyn) != 0;
     f.io(L.inv_dt0);
+    f.align4();
+    f.on = (mask & kGCont) != 0;
+    f.cont(Cont<C>::kWords);
     f.align4();
     f.on = (mask & kGRng) != 0;
     f.io64(L.st_hi); f.io64(L.st_lo); f.io64(L.inc_hi); f.io64(L.inc_lo);
@@ -289,6 +337,7 @@ MAS_HD void visit_state(EnvL<C>& L, F& f, uint32_t mask = kGAll)
 struct WordCounter {
     int n = 0;
     bool on = true;
+    MAS_HD void cont(int k) { n += k; }
     MAS_HD void align4() { n = (n + 3) & ~3; }
     template <class T> MAS_HD void io(T&) { n += 1; }
     template <class T> MAS_HD void io64(T&) { n += 2; }
@@ -469,10 +518,31 @@ MAS_HD StaticG static_geom(const EnvL<C>& L, const Params& P, int s)
 template <class C>
 MAS_HD StaticG static_geom_dyn(const EnvL<C>& L, const Params& P, int s)
 {
-    StaticG g = static_geom(L, P, 0);
+    // runtime s: select the raw inputs, then build the polygon once
+    StaticG g;
+    V2 wp = opq(P.wall_pos[0]);
+    Rot wq = P.wall_q[0];
+    float wa = P.wall_angle[0];
 #pragma unroll
-    for (int k = 1; k < C::NS; ++k) {
-        if (s == k) g = static_geom(L, P, k);
+    for (int k = 1; k < kNumWalls; ++k)
+        if (s == k) { wp = opq(P.wall_pos[k]); wq.s = opq(P.wall_q[k].s); wq.c = opq(P.wall_q[k].c); wa = opq(P.wall_angle[k]); }
+    const int b = s - kNumWalls;
+    V2 bp = opq(L.bp[0]);
+    float hx = opq(L.bhx[0]), hy = opq(L.bhy[0]);
+    int meta = opq(L.bmeta[0]);
+#pragma unroll
+    for (int k = 1; k < C::BM; ++k)
+        if (b == k) { bp = opq(L.bp[k]); hx = opq(L.bhx[k]); hy = opq(L.bhy[k]); meta = opq(L.bmeta[k]); }
+    if (s < kNumWalls) {
+        g.p = wp;
+        g.q = wq;
+        g.angle = wa;
+        g.poly = P.wall_poly;
+    } else {
+        g.p = bp;
+        g.q = kIdRot;
+        g.angle = 0.0f;
+        g.poly = box_poly(hx, hy, box_rot(meta), box_copied(meta));
     }
     return g;
 }

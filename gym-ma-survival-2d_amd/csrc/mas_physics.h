@@ -36,39 +36,19 @@ struct StepScratch {
 // ---------------------------------------------------------------------------
 // Collide: b2Contact::Update
 // ---------------------------------------------------------------------------
-template <class C, int I, int J>
-__device__ __forceinline__ void update_aa(EnvL<C>& L, const Params& P)
-{
-    constexpr int p = aa_index<C::AM>(I, J);
-    bool was = bit(L.aa_touch, p);
-    V2 d = sub(L.c[J], L.c[I]);
-    float dsq = dot(d, d);
-    float rad = P.agent_r + P.agent_r;
-    bool touching = !(dsq > rad * rad);
-    if (!(touching && was)) {
-        L.aa_ni[p] = 0.0f;
-        L.aa_ti[p] = 0.0f;
-    }
-    L.aa_touch = touching ? (L.aa_touch | (1u << p)) : (L.aa_touch & ~(1u << p));
-    if (touching != was) {
-        wake(L, I);
-        wake(L, J);
-    }
-}
-
 // polygon(A = static S) vs circle(B = agent I); returns touching, manifold out
 template <class C>
-__device__ __forceinline__ bool update_as_g(EnvL<C>& L, const Params& P, int I, int S, const StaticG& g, V2& ln,
-                                            V2& lp)
+__device__ __forceinline__ bool update_as_g(EnvL<C>& L, const Params& P, const Cont<C>& K, int I, int S,
+                                            const StaticG& g, V2& ln, V2& lp)
 {
-    uint32_t tm = sel(L.as_touch, I);
+    uint32_t tm = K.ast(I);
     bool was = bit(tm, S);
     bool touching = collide_pc(g.poly, g.p, g.q, sel(L.c, I), kPolyRadius, P.agent_r, ln, lp);
     if (!(touching && was)) {
-        put2(L.as_ni, I, S, 0.0f);
-        put2(L.as_ti, I, S, 0.0f);
+        K.set_asni(I, S, 0.0f);
+        K.set_asti(I, S, 0.0f);
     }
-    put(L.as_touch, I, touching ? (tm | (1u << S)) : (tm & ~(1u << S)));
+    K.set_ast(I, touching ? (tm | (1u << S)) : (tm & ~(1u << S)));
     if (touching != was) wake(L, I);
     return touching;
 }
@@ -266,7 +246,8 @@ __device__ __forceinline__ void static_pq(const EnvL<C>& L, const Params& P, int
 }
 
 template <class C>
-__device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScratch<C>& S, float h, float dtRatio)
+__device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const Cont<C>& K, StepScratch<C>& S, float h,
+                                            float dtRatio)
 {
     constexpr int AM = C::AM;
     const float m = P.inv_mass, I = P.inv_I;
@@ -274,8 +255,11 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
     int label[AM];
 #pragma unroll
     for (int i = 0; i < AM; ++i) label[i] = i;
+    // (agent-agent contacts are rare: the whole wave skips the propagation
+    // when none of its envs has one)
 #pragma unroll
     for (int pass = 0; pass < AM; ++pass) {
+        if (!__any(K.aat() != 0u)) continue;
 #pragma unroll
         for (int i = 0; i < AM; ++i)
 #pragma unroll
@@ -283,7 +267,7 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
                 constexpr int dummy = 0;
                 (void)dummy;
                 int p = aa_index<AM>(i, j);
-                if (bit(L.alive_m, i) && bit(L.alive_m, j) && bit(L.aa_touch, p)) {
+                if (bit(L.alive_m, i) && bit(L.alive_m, j) && bit(K.aat(), p)) {
                     int l = label[i] < label[j] ? label[i] : label[j];
                     label[i] = l;
                     label[j] = l;
@@ -325,11 +309,11 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
 #pragma unroll
         for (int j = i + 1; j < AM; ++j) {
             int p = aa_index<AM>(i, j);
-            if (bit(solved, i) && bit(solved, j) && bit(L.aa_touch, p)) {
+            if (bit(solved, i) && bit(solved, j) && bit(K.aat(), p)) {
                 if (sl.n < C::KC) {
                     VC k = vc_init_aa(L.c[i], L.c[j], P.agent_r, m, I, m, I);
-                    k.ni = dtRatio * L.aa_ni[p];
-                    k.ti = dtRatio * L.aa_ti[p];
+                    k.ni = dtRatio * K.aani(p);
+                    k.ti = dtRatio * K.aati(p);
                     int key = (0 << 16) | (i << 8) | j;
 #pragma unroll
                     for (int q = 0; q < C::KC; ++q)
@@ -340,17 +324,20 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
         }
 #pragma unroll
     for (int i = 0; i < AM; ++i) {
-        if (!bit(solved, i)) continue;
-#pragma unroll
-        for (int s = 0; s < C::NS; ++s) {
-            if (!bit(L.as_touch[i], s)) continue;
+        uint32_t t = bit(solved, i) ? K.ast(i) : 0u;
+        // touching statics of agent i in canonical order (per-lane loop: the
+        // trip count is the lane's contact count, usually 0)
+#pragma unroll 1
+        while (t) {
+            const int s = __builtin_ctz(t);
+            t &= t - 1;
             if (sl.n < C::KC) {
-                StaticG g = static_geom(L, P, s);
+                StaticG g = static_geom_dyn(L, P, s);
                 V2 ln = mk(0.0f, 0.0f), lp = mk(0.0f, 0.0f);
                 collide_pc(g.poly, g.p, g.q, L.c[i], kPolyRadius, P.agent_r, ln, lp);
                 VC k = vc_init_as(g.p, g.q, ln, lp, L.c[i], P.agent_r, m, I);
-                k.ni = dtRatio * L.as_ni[i][s];
-                k.ti = dtRatio * L.as_ti[i][s];
+                k.ni = dtRatio * K.asni(i, s);
+                k.ti = dtRatio * K.asti(i, s);
                 int key = (1 << 16) | (i << 8) | s;
 #pragma unroll
                 for (int q = 0; q < C::KC; ++q)
@@ -362,9 +349,10 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
     overflow = sl.n > C::KC;
     if (!overflow) {
         // ---------------- fast path: compact slots ----------------
-        // warm start
+        // warm start (slot loops: the wave skips slots none of its envs uses)
 #pragma unroll
         for (int q = 0; q < C::KC; ++q) {
+            if (!__any(q < sl.n)) continue;
             if (q >= sl.n) continue;
             int key = sl.key[q];
             int i = slot_i(key), js = slot_js(key);
@@ -383,8 +371,10 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
             }
         }
         for (int it = 0; it < 10; ++it) {
+            if (!__any(sl.n > 0)) break;
 #pragma unroll
             for (int q = 0; q < C::KC; ++q) {
+                if (!__any(q < sl.n)) continue;
                 if (q >= sl.n) continue;
                 int key = sl.key[q];
                 int i = slot_i(key), js = slot_js(key);
@@ -406,27 +396,16 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
         // store impulses
 #pragma unroll
         for (int q = 0; q < C::KC; ++q) {
+            if (!__any(q < sl.n)) continue;
             if (q >= sl.n) continue;
             int key = sl.key[q];
             int i = slot_i(key), js = slot_js(key);
             if (slot_type(key) == 0) {
-#pragma unroll
-                for (int a = 0; a < AM; ++a)
-#pragma unroll
-                    for (int b = a + 1; b < AM; ++b)
-                        if (a == i && b == js) {
-                            L.aa_ni[aa_index<AM>(a, b)] = sl.k[q].ni;
-                            L.aa_ti[aa_index<AM>(a, b)] = sl.k[q].ti;
-                        }
+                K.set_aani(aa_index<AM>(i, js), sl.k[q].ni);
+                K.set_aati(aa_index<AM>(i, js), sl.k[q].ti);
             } else {
-#pragma unroll
-                for (int a = 0; a < AM; ++a)
-#pragma unroll
-                    for (int s = 0; s < C::NS; ++s)
-                        if (a == i && s == js) {
-                            L.as_ni[a][s] = sl.k[q].ni;
-                            L.as_ti[a][s] = sl.k[q].ti;
-                        }
+                K.set_asni(i, js, sl.k[q].ni);
+                K.set_asti(i, js, sl.k[q].ti);
             }
         }
     } else {
@@ -443,11 +422,11 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
 #pragma unroll 1
                 for (int j = i + 1; j < AM; ++j) {
                     int p = aa_index<AM>(i, j);
-                    if (!(bit(solved, i) && bit(solved, j) && bit(L.aa_touch, p))) continue;
-                    float ni = sel(L.aa_ni, p), ti = sel(L.aa_ti, p);
+                    if (!(bit(solved, i) && bit(solved, j) && bit(K.aat(), p))) continue;
+                    float ni = K.aani(p), ti = K.aati(p);
                     if (it == -2) {
-                        put(L.aa_ni, p, dtRatio * ni);
-                        put(L.aa_ti, p, dtRatio * ti);
+                        K.set_aani(p, dtRatio * ni);
+                        K.set_aati(p, dtRatio * ti);
                         continue;
                     }
                     VC k = vc_init_aa(sel(cpos, i), sel(cpos, j), P.agent_r, m, I, m, I);
@@ -459,21 +438,21 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
                     else vc_solve(k, vA, wA, vB, wB, m, I, m, I);
                     put(L.v, i, vA); put(L.w, i, wA);
                     put(L.v, j, vB); put(L.w, j, wB);
-                    put(L.aa_ni, p, k.ni);
-                    put(L.aa_ti, p, k.ti);
+                    K.set_aani(p, k.ni);
+                    K.set_aati(p, k.ti);
                 }
             }
 #pragma unroll 1
             for (int i = 0; i < AM; ++i) {
                 if (!bit(solved, i)) continue;
-                uint32_t tm = sel(L.as_touch, i);
+                uint32_t tm = K.ast(i);
 #pragma unroll 1
                 for (int s = 0; s < C::NS; ++s) {
                     if (!bit(tm, s)) continue;
-                    float ni = sel2(L.as_ni, i, s), ti = sel2(L.as_ti, i, s);
+                    float ni = K.asni(i, s), ti = K.asti(i, s);
                     if (it == -2) {
-                        put2(L.as_ni, i, s, dtRatio * ni);
-                        put2(L.as_ti, i, s, dtRatio * ti);
+                        K.set_asni(i, s, dtRatio * ni);
+                        K.set_asti(i, s, dtRatio * ti);
                         continue;
                     }
                     StaticG g = static_geom_dyn(L, P, s);
@@ -488,8 +467,8 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
                     if (it < 0) vc_warm(k, vz, wz, vB, wB, 0.0f, 0.0f, m, I);
                     else vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, I);
                     put(L.v, i, vB); put(L.w, i, wB);
-                    put2(L.as_ni, i, s, k.ni);
-                    put2(L.as_ti, i, s, k.ti);
+                    K.set_asni(i, s, k.ni);
+                    K.set_asti(i, s, k.ti);
                 }
             }
         }
@@ -508,6 +487,7 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
         if (!overflow) {
 #pragma unroll
             for (int q = 0; q < C::KC; ++q) {
+                if (!__any(q < sl.n)) continue;
                 if (q >= sl.n) continue;
                 int key = sl.key[q];
                 int i = slot_i(key), js = slot_js(key);
@@ -539,7 +519,7 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
 #pragma unroll 1
                 for (int j = i + 1; j < AM; ++j) {
                     int p = aa_index<AM>(i, j);
-                    if (!(bit(solved, i) && bit(solved, j) && bit(L.aa_touch, p))) continue;
+                    if (!(bit(solved, i) && bit(solved, j) && bit(K.aat(), p))) continue;
                     int root = sel(label, i);
                     if (bit(done_isl, root)) continue;
                     V2 cA = sel(L.c, i), cB = sel(L.c, j);
@@ -552,7 +532,7 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, StepScr
 #pragma unroll 1
             for (int i = 0; i < AM; ++i) {
                 if (!bit(solved, i)) continue;
-                uint32_t tm = sel(L.as_touch, i);
+                uint32_t tm = K.ast(i);
                 int root = sel(label, i);
 #pragma unroll 1
                 for (int s = 0; s < C::NS; ++s) {
@@ -1026,7 +1006,8 @@ MAS_HD bool toi_reject(const StaticG& g, V2 p0, V2 p1, float rB)
 // b2World::SolveTOI for agent I (events of different agents are independent:
 // statics never move and agent-agent pairs are not TOI pairs).
 template <class C>
-__device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const StepScratch<C>& S, int I, float dt)
+__device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const Cont<C>& K, const StepScratch<C>& S, int I,
+                                          float dt)
 {
     const float m = P.inv_mass, Ii = P.inv_I;
     Sweep sw;
@@ -1098,7 +1079,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const Ste
         put(L.a, I, sw.a);
         StaticG gm = static_geom_dyn(L, P, minS);
         V2 lnm = mk(0.0f, 0.0f), lpm = mk(0.0f, 0.0f);
-        bool touching = update_as_g(L, P, I, minS, gm, lnm, lpm);
+        bool touching = update_as_g(L, P, K, I, minS, gm, lnm, lpm);
         valid &= ~(1u << minS);
 #pragma unroll
         for (int s = 0; s < C::NS; ++s)
@@ -1121,7 +1102,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const Ste
             if (s >= ns || s == minS) continue;
             enabled |= 1u << s;
             StaticG g = static_geom(L, P, s);
-            if (update_as_g(L, P, I, s, g, iln[s], ilp[s])) isl |= 1u << s;
+            if (update_as_g(L, P, K, I, s, g, iln[s], ilp[s])) isl |= 1u << s;
         }
         // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
         V2 cB = sel(L.c, I);
@@ -1185,9 +1166,118 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const Ste
     put(L.a, I, sw.a);
 }
 
+
+// ---------------------------------------------------------------------------
+// Contact-free fast path of one world.Step (speculative).  Valid while the
+// env has no contact memory, no pair reaches touching distance and no TOI
+// sweep can hit a static: then Box2D's step is damping + integrate + sleep
+// per agent, which this function computes with the same operations in the
+// same order as world_step / world_solve.  Anything else (a contact, a
+// candidate narrowphase pair, a TOI sweep the cheap test cannot reject) sets
+// `bail`: the caller discards the registers and the env is re-run by the
+// general kernel.  Returns false on bail.
+// ---------------------------------------------------------------------------
+template <class C>
+__device__ __forceinline__ bool world_step_fast(EnvL<C>& L, const Params& P, float dt)
+{
+    V2 c0[C::AM];
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) c0[i] = L.c[i];
+    const float inv_dt = dt > 0.0f ? 1.0f / dt : 0.0f;
+    // Collide: any agent-agent pair at touching distance -> general path
+    bool bail = false;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+#pragma unroll
+        for (int j = i + 1; j < C::AM; ++j) {
+            if (!(bit(L.alive_m, i) && bit(L.alive_m, j))) continue;
+            if (!(bit(L.awake_m, i) || bit(L.awake_m, j))) continue;
+            V2 d = sub(L.c[j], L.c[i]);
+            float rad = P.agent_r + P.agent_r;
+            if (!(dot(d, d) > rad * rad)) bail = true;
+        }
+    // agent-static pairs: any narrowphase candidate -> general path
+    const int ns = kNumWalls + L.nbox;
+    const float reach = P.agent_r + kPolyRadius + 1e-3f;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (s >= ns) continue;
+            V2 lo, hi;
+            if (s < kNumWalls) {
+                lo = P.wall_lo[s];
+                hi = P.wall_hi[s];
+            } else {
+                const int b = s - kNumWalls;
+                lo = mk(L.bp[b].x - L.bhx[b], L.bp[b].y - L.bhy[b]);
+                hi = mk(L.bp[b].x + L.bhx[b], L.bp[b].y + L.bhy[b]);
+            }
+            const float dx = fmaxf(fmaxf(lo.x - L.c[i].x, L.c[i].x - hi.x), 0.0f);
+            const float dy = fmaxf(fmaxf(lo.y - L.c[i].y, L.c[i].y - hi.y), 0.0f);
+            if (dx * dx + dy * dy <= reach * reach) bail = true;
+        }
+    }
+    if (bail) return false;
+    // Solve: every awake alive agent is its own island (world_solve with no
+    // contacts: damping, integrate, one position pass that is already done,
+    // per-island sleep)
+    const float h = dt;
+    uint32_t solved = 0;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+        if (bit(L.alive_m, i) && bit(L.awake_m, i)) solved |= 1u << i;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!bit(solved, i)) continue;
+        float ld = 1.0f / (1.0f + h * P.lin_damp);
+        L.v[i].x *= ld;
+        L.v[i].y *= ld;
+        float ad = 1.0f / (1.0f + h * P.ang_damp);
+        L.w[i] *= ad;
+    }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+        if (bit(solved, i)) integrate(L.c[i], L.a[i], L.v[i], L.w[i], h);
+    const float linTolSqr = kLinSleepTol * kLinSleepTol;
+    const float angTolSqr = kAngSleepTol * kAngSleepTol;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!bit(solved, i)) continue;
+        float ms;
+        if (L.w[i] * L.w[i] > angTolSqr || dot(L.v[i], L.v[i]) > linTolSqr) {
+            L.sleep[i] = 0.0f;
+            ms = 0.0f;
+        } else {
+            L.sleep[i] += h;
+            ms = fmin_b2(kMaxFloat, L.sleep[i]);
+        }
+        if (ms >= kTimeToSleep) {
+            L.awake_m &= ~(1u << i);
+            L.sleep[i] = 0.0f;
+            L.v[i] = mk(0.0f, 0.0f);
+            L.w[i] = 0.0f;
+        }
+    }
+    // SolveTOI: every sweep of an awake agent must be rejected by the cheap test
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) {
+        if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (s >= ns) continue;
+            StaticG g = static_geom(L, P, s);
+            if (!toi_reject(g, c0[i], L.c[i], P.agent_r)) bail = true;
+        }
+    }
+    L.inv_dt0 = inv_dt;
+    return !bail;
+}
+
 // b2World::Step(dt, 10, 10)
 template <class C>
-__device__ __forceinline__ void world_step(EnvL<C>& L, const Params& P, float dt)
+__device__ __forceinline__ void world_step(EnvL<C>& L, const Params& P, const Cont<C>& K, float dt)
 {
     StepScratch<C> S;
 #pragma unroll
@@ -1205,39 +1295,75 @@ __device__ __forceinline__ void world_step(EnvL<C>& L, const Params& P, float dt
             if (!(bit(L.alive_m, i) && bit(L.alive_m, j))) continue;
             if (!(bit(L.awake_m, i) || bit(L.awake_m, j))) continue;
             int p = aa_index<C::AM>(i, j);
-            bool was = bit(L.aa_touch, p);
+            const uint32_t at = K.aat();
+            bool was = bit(at, p);
             V2 d = sub(L.c[j], L.c[i]);
             float dsq = dot(d, d);
             float rad = P.agent_r + P.agent_r;
             bool touching = !(dsq > rad * rad);
             if (!(touching && was)) {
-                L.aa_ni[p] = 0.0f;
-                L.aa_ti[p] = 0.0f;
+                K.set_aani(p, 0.0f);
+                K.set_aati(p, 0.0f);
             }
-            L.aa_touch = touching ? (L.aa_touch | (1u << p)) : (L.aa_touch & ~(1u << p));
+            K.set_aat(touching ? (at | (1u << p)) : (at & ~(1u << p)));
             if (touching != was) {
                 wake(L, i);
                 wake(L, j);
             }
         }
+    // agent-static pairs: the exact b2CollidePolygonAndCircle runs only for
+    // pairs a cheap test cannot rule out (circle vs the static's AABB, with a
+    // margin): a pair beyond it has separation > radius, so the exact result
+    // would be "not touching".  Those pairs are updated with mask arithmetic
+    // (impulses reset, wake on a lost contact) -- the same state changes
+    // b2Contact::Update makes -- and the survivors go through the exact update
+    // in a per-lane loop whose trip count is the lane's survivor count.
     const int ns = kNumWalls + L.nbox;
+    const float reach = P.agent_r + kPolyRadius + 1e-3f;
 #pragma unroll
     for (int i = 0; i < C::AM; ++i) {
         if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
+        const V2 ci = L.c[i];
+        uint32_t cand = 0;
 #pragma unroll
         for (int s = 0; s < C::NS; ++s) {
             if (s >= ns) continue;
-            StaticG g = static_geom(L, P, s);
+            V2 lo, hi;
+            if (s < kNumWalls) {
+                lo = P.wall_lo[s];
+                hi = P.wall_hi[s];
+            } else {
+                const int b = s - kNumWalls;
+                lo = mk(L.bp[b].x - L.bhx[b], L.bp[b].y - L.bhy[b]);
+                hi = mk(L.bp[b].x + L.bhx[b], L.bp[b].y + L.bhy[b]);
+            }
+            const float dx = fmaxf(fmaxf(lo.x - ci.x, ci.x - hi.x), 0.0f);
+            const float dy = fmaxf(fmaxf(lo.y - ci.y, ci.y - hi.y), 0.0f);
+            if (dx * dx + dy * dy <= reach * reach) cand |= 1u << s;
+        }
+        const uint32_t lost = K.ast(i) & ~cand;
+        if (lost) {
+            wake(L, i);
+#pragma unroll
+            for (int s = 0; s < C::NS; ++s)
+                if (bit(lost, s)) { K.set_asni(i, s, 0.0f); K.set_asti(i, s, 0.0f); }
+            K.set_ast(i, K.ast(i) & cand);
+        }
+#pragma unroll 1
+        while (cand) {
+            const int s = __builtin_ctz(cand);
+            cand &= cand - 1;
+            StaticG g = static_geom_dyn(L, P, s);
             V2 ln, lp;
-            update_as_g(L, P, i, s, g, ln, lp);
+            update_as_g(L, P, K, i, s, g, ln, lp);
         }
     }
     MAS_PROF(P, kPfCollide);
-    world_solve(L, P, S, dt, dtRatio);
+    world_solve(L, P, K, S, dt, dtRatio);
     MAS_PROF(P, kPfSolve);
     for (int i = 0; i < C::AM; ++i) {  // runtime loop: toi_agent indexes agents via sel/put
         if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
-        toi_agent(L, P, S, i, dt);
+        toi_agent(L, P, K, S, i, dt);
     }
     MAS_PROF(P, kPfToi);
     L.inv_dt0 = inv_dt;

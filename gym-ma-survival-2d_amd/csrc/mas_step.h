@@ -579,16 +579,7 @@ __device__ __forceinline__ void env_reset(EnvL<C>& L, const Params& P, Scr<C>& s
         cj = P.floor_size * cj - P.floor_size / 2.0;
         return mk((float)ci, (float)cj);
     };
-    // new b2World: no contacts, inv_dt0 = 0
-    L.aa_touch = 0;
-#pragma unroll
-    for (int p = 0; p < (C::NAA > 0 ? C::NAA : 1); ++p) { L.aa_ni[p] = 0.0f; L.aa_ti[p] = 0.0f; }
-#pragma unroll
-    for (int i = 0; i < C::AM; ++i) {
-        L.as_touch[i] = 0;
-#pragma unroll
-        for (int s = 0; s < C::NS; ++s) { L.as_ni[i][s] = 0.0f; L.as_ti[i][s] = 0.0f; }
-    }
+    // new b2World: no contacts (k_reset zeroes the contact memory), inv_dt0 = 0
     L.inv_dt0 = 0.0f;
     // boxes: RandomizeBoxShapes (semantics.py:107-120), ResetSpawns, Health
     L.nbox = 0;
@@ -856,12 +847,12 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
 }
 
 template <class C>
-__device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P)
+__device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P, const Cont<C>& K)
 {
     // ---------------- physics: 2 x world.Step(1/60, 10, 10) ----------------
     const float dt = (float)(1.0 / 60.0);
 #pragma unroll 1
-    for (int k = 0; k < 2; ++k) world_step(L, P, dt);
+    for (int k = 0; k < 2; ++k) world_step(L, P, K, dt);
     // ---------------- post_step ----------------
     // boxes: Health.post_step + Object / OwnedObject despawn (semantics.py:429-435, 858-861, 907-912)
     {
@@ -900,11 +891,11 @@ __device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P)
                         L.bp[k] = p; L.bhx[k] = hx; L.bhy[k] = hy; L.bmeta[k] = meta; L.bhealth[k] = hl;
 #pragma unroll
                         for (int i = 0; i < C::AM; ++i) {
-                            bool tb = bit(L.as_touch[i], kNumWalls + b);
-                            L.as_touch[i] = tb ? (L.as_touch[i] | (1u << (kNumWalls + k)))
-                                               : (L.as_touch[i] & ~(1u << (kNumWalls + k)));
-                            L.as_ni[i][kNumWalls + k] = L.as_ni[i][kNumWalls + b];
-                            L.as_ti[i][kNumWalls + k] = L.as_ti[i][kNumWalls + b];
+                            const uint32_t at = K.ast(i);
+                            bool tb = bit(at, kNumWalls + b);
+                            K.set_ast(i, tb ? (at | (1u << (kNumWalls + k))) : (at & ~(1u << (kNumWalls + k))));
+                            K.set_asni(i, kNumWalls + k, K.asni(i, kNumWalls + b));
+                            K.set_asti(i, kNumWalls + k, K.asti(i, kNumWalls + b));
                         }
                     }
                     ++wi;
@@ -916,9 +907,9 @@ __device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P)
                 if (k < wi) continue;
 #pragma unroll
                 for (int i = 0; i < C::AM; ++i) {
-                    L.as_touch[i] &= ~(1u << (kNumWalls + k));
-                    L.as_ni[i][kNumWalls + k] = 0.0f;
-                    L.as_ti[i][kNumWalls + k] = 0.0f;
+                    K.set_ast(i, K.ast(i) & ~(1u << (kNumWalls + k)));
+                    K.set_asni(i, kNumWalls + k, 0.0f);
+                    K.set_asti(i, kNumWalls + k, 0.0f);
                 }
             }
         }
@@ -928,7 +919,7 @@ __device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P)
 // agents: Cameras.post_step over the pre-despawn list runs between step_phys
 // and step_post (k_cameras); step_post reads and compacts its bytes.
 template <class C>
-__device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, float* rew)
+__device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const Cont<C>& K, float* rew)
 {
     const int A = P.A;
     // agents: Health.post_step -> despawn dead (id order): TrackDeaths, IndexBodies,
@@ -977,16 +968,16 @@ __device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, float* re
             kill_cause[i] = L.cause[i];
             L.alive_m &= ~(1u << i);
             L.awake_m &= ~(1u << i);
-            L.as_touch[i] = 0;
+            K.set_ast(i, 0u);
 #pragma unroll
-            for (int s = 0; s < C::NS; ++s) { L.as_ni[i][s] = 0.0f; L.as_ti[i][s] = 0.0f; }
+            for (int s = 0; s < C::NS; ++s) { K.set_asni(i, s, 0.0f); K.set_asti(i, s, 0.0f); }
 #pragma unroll
             for (int j = 0; j < C::AM; ++j) {
                 if (j == i) continue;
                 int p = j < i ? aa_index<C::AM>(j, i) : aa_index<C::AM>(i, j);
-                L.aa_touch &= ~(1u << p);
-                L.aa_ni[p] = 0.0f;
-                L.aa_ti[p] = 0.0f;
+                K.set_aat(K.aat() & ~(1u << p));
+                K.set_aani(p, 0.0f);
+                K.set_aati(p, 0.0f);
             }
         }
     }

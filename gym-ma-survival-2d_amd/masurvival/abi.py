@@ -60,6 +60,7 @@ SIGNATURES = {
     'mas_set_state': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'mas_gae': (c_int32, [c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
                           c_void_p, c_void_p, c_void_p, c_void_p]),
+    'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_last_error': (c_char_p, []),
     'mas_abi_version': (c_int32, []),
 }

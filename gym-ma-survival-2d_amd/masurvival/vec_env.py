@@ -129,6 +129,13 @@ class VecMaSurvival:
             out[k] = flat[..., off:off + size].reshape(*flat.shape[:-1], *shp)
         return out
 
+    def debug_counters(self):
+        """{'phys_general_envs': envs of the last step that ran the general
+        physics kernel (left the contact-free fast path)}; synchronises."""
+        out = (ctypes.c_int64 * 1)()
+        check(self._lib.mas_debug_counters(self._h, out))
+        return {'phys_general_envs': int(out[0])}
+
     def state_bytes(self) -> int:
         return int(self._lib.mas_state_bytes(self._h))
 

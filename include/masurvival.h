@@ -152,6 +152,11 @@ int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards
             const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
             void* stream);
 
+/* Diagnostics (synchronises the device): host_out[0] = envs of the last
+ * mas_step that left the contact-free physics fast path and ran the general
+ * physics kernel (contacts, TOI events, box despawns). */
+int mas_debug_counters(mas_handle* h, int64_t* host_out);
+
 const char* mas_last_error(void);
 int32_t mas_abi_version(void);
 

@@ -57,7 +57,8 @@ typedef ora_poly poly;
 
 /* coverage counters (tests assert the golden fixtures exercise each path) */
 enum { CNT_TOI_EVENT, CNT_TOI_RESTORE, CNT_SLEEP, CNT_BOX_BROKEN, CNT_BOX_PLACED, CNT_ITEM_PICKED,
-       CNT_GIVE_OK, CNT_GIVE_LOST, CNT_DROP_ITEMS, CNT_HEAL_USED, CNT_DOUBLE_PICK, CNT_AA_CONTACT, CNT_N };
+       CNT_GIVE_OK, CNT_GIVE_LOST, CNT_DROP_ITEMS, CNT_HEAL_USED, CNT_DOUBLE_PICK, CNT_AA_CONTACT,
+       CNT_ISLAND_K, CNT_ISLANDS, CNT_ISLAND_K_GT2, CNT_ISLAND_K_GT4, CNT_ISLAND_K_GT8, CNT_N };
 static __thread int64_t g_cnt[CNT_N];
 void ora_counters(int64_t* out, int32_t reset)
 {
@@ -1072,6 +1073,11 @@ static void world_solve(ora_world* w, step_scratch* sc, float h, float dtRatio, 
             float ad = 1.0f / (1.0f + h * w->ang_damp);
             w->w[i] *= ad;
         }
+        g_cnt[CNT_ISLANDS]++;
+        g_cnt[CNT_ISLAND_K] += nk;
+        if (nk > 2) g_cnt[CNT_ISLAND_K_GT2]++;
+        if (nk > 4) g_cnt[CNT_ISLAND_K_GT4]++;
+        if (nk > 8) g_cnt[CNT_ISLAND_K_GT8]++;
         for (int q = 0; q < nk; ++q) init_vcon(w, &ks[q], dtRatio, 1);
         for (int q = 0; q < nk; ++q) warm_start(w, &ks[q]);
         for (int it = 0; it < vel_iters; ++it)

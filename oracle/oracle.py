@@ -46,7 +46,8 @@ def lib():
 
 
 COUNTER_NAMES = ['toi_event', 'toi_restore', 'sleep', 'box_broken', 'box_placed', 'item_picked', 'give_ok',
-                 'give_lost', 'drop_items', 'heal_used', 'double_pick', 'aa_contact']
+                 'give_lost', 'drop_items', 'heal_used', 'double_pick', 'aa_contact', 'island_contacts', 'islands',
+                 'islands_k_gt2', 'islands_k_gt4', 'islands_k_gt8']
 
 
 def counters(reset=True):

@@ -38,13 +38,15 @@ def main():
     for _ in range(5):
         env.step(acts())
     abi.check(lib.mas_prof_read(env._h, buf))
+    active_waves = 0
     for _ in range(steps):
         env.step(acts())
+        active_waves += (env.debug_counters()['phys_general_envs'] + 63) // 64
     abi.check(lib.mas_prof_read(env._h, buf))
-    waves = (n + 63) // 64
+    waves = active_waves / steps  # k_phys (general path) runs only the envs that left the fast path
     t = np.array(buf[:len(PHASES)], dtype=np.float64) * 0.01 / (waves * steps)  # us per wave-step
     top = t.sum()
-    print(f'# k_phys phase times, {cfg_name} N={n}, mean per wave per step (us); total {top:.1f} us')
+    print(f'# k_phys (general path) phase times, {cfg_name} N={n}, {waves:.1f} active waves/step, mean per active wave per step (us); total {top:.1f} us')
     for name, v in zip(PHASES, t):
         print(f'{name:32s} {v:9.2f} us  {100 * v / top:5.1f}%')
 
