@@ -75,6 +75,7 @@ def main():
                     help='ppo: policy forward + env step + buffer, GAE + PPO update every horizon; env: random actions')
     ap.add_argument('--horizon', type=int, default=64)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--lib', default=None, help='alternative libmas*.so (A/B variants)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -84,6 +85,9 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
 
+    if args.lib:
+        from masurvival import abi
+        abi.load_library(args.lib)
     from masurvival.config import NAMED_CONFIGS
     from masurvival.vec_env import VecMaSurvival
     cfg = NAMED_CONFIGS[args.config]

@@ -221,7 +221,8 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
-    int* phys;  // [N] env list + [1] count (k_phys_fast -> k_phys)
+    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path)
+    float* sweep;
     mas_obs_layout layout;
 };
 
@@ -427,6 +428,9 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->phys = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 1) * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 1) * sizeof(int));
+    h->sweep = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * 8 * sizeof(float));
+    h->P.sweep = h->sweep;
     h->P.phys_list = h->phys;
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
 #ifdef MAS_PROFILE
@@ -450,6 +454,7 @@ int mas_destroy(mas_handle* h)
     if (h->seedbuf) hipFree(h->seedbuf);
     if (h->P.prof) (void)hipFree(h->P.prof);
     if (h->phys) (void)hipFree(h->phys);
+    if (h->sweep) (void)hipFree(h->sweep);
     delete h;
     return MAS_OK;
 }

@@ -75,6 +75,7 @@ struct Params {
     int o_agent, o_bi, o_bim, o_bs, o_bsm, o_box, o_boxm, o_hs, o_hsm, o_heal, o_healm, o_oth, o_othm, o_zone;
     int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
     int* phys_count;  // number of them
+    float* sweep;     // [list position][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
 
@@ -151,14 +152,36 @@ constexpr int kLanes = 64;  // one wave per workgroup in every env kernel
 // (k_phys, k_post, k_reset): every access is by runtime pair index at LDS
 // cost instead of a select over the whole table in registers.  The HBM image
 // holds the same words in the same order (state group kGCont).
+#ifndef MAS_STATE_VEC4
+#define MAS_STATE_VEC4 0
+#endif
+#if MAS_STATE_VEC4
+MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (((int64_t)(w >> 2)) * N + e) * 4 + (w & 3); }
+#else
+MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (int64_t)w * N + e; }
+#endif
+
 template <class C>
-struct Cont {
-    static constexpr int kNAA = C::NAA > 0 ? C::NAA : 1;
-    static constexpr int kAAT = 0, kAST = 1, kAANI = 1 + C::AM, kAATI = kAANI + kNAA, kASNI = kAATI + kNAA,
-                         kASTI = kASNI + C::AM * C::NS, kWords = kASTI + C::AM * C::NS;
+struct ContLdsStore {  // [word][kLanes] in LDS
     uint32_t* u;
     int tid;
     MAS_HD uint32_t& w(int k) const { return u[k * kLanes + tid]; }
+};
+
+template <class C>
+struct ContGlbStore {  // the kGCont words of the HBM image (rare paths)
+    uint32_t* st;
+    int64_t N, e;
+    int w0;
+    MAS_HD uint32_t& w(int k) const { return st[state_index(w0 + k, e, N)]; }
+};
+
+template <class C, class S = ContLdsStore<C>>
+struct Cont : S {
+    static constexpr int kNAA = C::NAA > 0 ? C::NAA : 1;
+    static constexpr int kAAT = 0, kAST = 1, kAANI = 1 + C::AM, kAATI = kAANI + kNAA, kASNI = kAATI + kNAA,
+                         kASTI = kASNI + C::AM * C::NS, kWords = kASTI + C::AM * C::NS;
+    using S::w;
     MAS_HD uint32_t aat() const { return w(kAAT); }
     MAS_HD void set_aat(uint32_t v) const { w(kAAT) = v; }
     MAS_HD uint32_t ast(int i) const { return w(kAST + i); }
@@ -171,10 +194,6 @@ struct Cont {
     MAS_HD float asti(int i, int s) const { return bits_f(w(kASTI + i * C::NS + s)); }
     MAS_HD void set_asni(int i, int s, float v) const { w(kASNI + i * C::NS + s) = f_bits(v); }
     MAS_HD void set_asti(int i, int s, float v) const { w(kASTI + i * C::NS + s) = f_bits(v); }
-    MAS_HD void clear() const
-    {
-        for (int k = 0; k < kWords; ++k) w(k) = 0u;
-    }
     MAS_HD static float bits_f(uint32_t u)
     {
         float f;
@@ -189,14 +208,7 @@ struct Cont {
     }
 };
 
-#ifndef MAS_STATE_VEC4
-#define MAS_STATE_VEC4 0
-#endif
-#if MAS_STATE_VEC4
-MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (((int64_t)(w >> 2)) * N + e) * 4 + (w & 3); }
-#else
-MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (int64_t)w * N + e; }
-#endif
+
 
 template <class C>
 struct EnvL {

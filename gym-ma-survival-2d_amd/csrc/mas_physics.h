@@ -37,8 +37,8 @@ struct StepScratch {
 // Collide: b2Contact::Update
 // ---------------------------------------------------------------------------
 // polygon(A = static S) vs circle(B = agent I); returns touching, manifold out
-template <class C>
-__device__ __forceinline__ bool update_as_g(EnvL<C>& L, const Params& P, const Cont<C>& K, int I, int S,
+template <class C, class KT>
+__device__ __forceinline__ bool update_as_g(EnvL<C>& L, const Params& P, const KT& K, int I, int S,
                                             const StaticG& g, V2& ln, V2& lp)
 {
     uint32_t tm = K.ast(I);
@@ -1005,8 +1005,8 @@ MAS_HD bool toi_reject(const StaticG& g, V2 p0, V2 p1, float rB)
 
 // b2World::SolveTOI for agent I (events of different agents are independent:
 // statics never move and agent-agent pairs are not TOI pairs).
-template <class C>
-__device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const Cont<C>& K, const StepScratch<C>& S, int I,
+template <class C, class KT>
+__device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT& K, const StepScratch<C>& S, int I,
                                           float dt)
 {
     const float m = P.inv_mass, Ii = P.inv_I;
@@ -1275,11 +1275,15 @@ __device__ __forceinline__ bool world_step_fast(EnvL<C>& L, const Params& P, flo
     return !bail;
 }
 
-// b2World::Step(dt, 10, 10)
+// b2World::Step(dt, 10, 10) up to SolveTOI: Collide + Solve.  S returns the
+// sweep start (b2Sweep c0/a0) of every agent for SolveTOI, which runs as its
+// own kernel, one lane per (env, agent) (k_gen_toi): TOI events of different
+// agents are independent (statics never move, agent-agent pairs are not TOI
+// pairs, and every agent SolveTOI touches is already awake).
 template <class C>
-__device__ __forceinline__ void world_step(EnvL<C>& L, const Params& P, const Cont<C>& K, float dt)
+__device__ __forceinline__ void world_step_solve(EnvL<C>& L, const Params& P, const Cont<C>& K, float dt,
+                                                 StepScratch<C>& S)
 {
-    StepScratch<C> S;
 #pragma unroll
     for (int i = 0; i < C::AM; ++i) {
         S.c0[i] = L.c[i];
@@ -1361,11 +1365,6 @@ __device__ __forceinline__ void world_step(EnvL<C>& L, const Params& P, const Co
     MAS_PROF(P, kPfCollide);
     world_solve(L, P, K, S, dt, dtRatio);
     MAS_PROF(P, kPfSolve);
-    for (int i = 0; i < C::AM; ++i) {  // runtime loop: toi_agent indexes agents via sel/put
-        if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
-        toi_agent(L, P, K, S, i, dt);
-    }
-    MAS_PROF(P, kPfToi);
     L.inv_dt0 = inv_dt;
 }
 

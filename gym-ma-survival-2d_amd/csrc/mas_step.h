@@ -846,15 +846,15 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
     L.stats[18] += (float)uses_box;
 }
 
-template <class C>
-__device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P, const Cont<C>& K)
+// boxes: Health.post_step + Object / OwnedObject despawn (semantics.py:429-435,
+// 858-861, 907-912) -- the first post_step hook (dict order: boxes group
+// before agents), run at the start of k_cameras.  Returns true when the box /
+// pending groups changed.  KT: contact-memory accessor (despawn compaction
+// shifts the agent-static contact rows).
+template <class C, class KT>
+__device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT& K)
 {
-    // ---------------- physics: 2 x world.Step(1/60, 10, 10) ----------------
-    const float dt = (float)(1.0 / 60.0);
-#pragma unroll 1
-    for (int k = 0; k < 2; ++k) world_step(L, P, K, dt);
-    // ---------------- post_step ----------------
-    // boxes: Health.post_step + Object / OwnedObject despawn (semantics.py:429-435, 858-861, 907-912)
+    bool changed = false;
     {
         bool any_dead = false;
 #pragma unroll
@@ -864,10 +864,12 @@ __device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P, const Con
             if (!box_hinit(meta)) {
                 L.bmeta[b] = mk_boxmeta(box_rot(meta), box_copied(meta), 1, box_vuln(meta), box_cause(meta));
                 L.bhealth[b] = P.box_health;
+                changed = true;
             }
             if (L.bhealth[b] <= 0) any_dead = true;
         }
         if (any_dead) {
+            changed = true;
             // stable compaction; dead boxes queue (pos, copy_shape(proto), cause)
             int wi = 0;
 #pragma unroll
@@ -914,6 +916,7 @@ __device__ __forceinline__ void step_phys(EnvL<C>& L, const Params& P, const Con
             }
         }
     }
+    return changed;
 }
 
 // agents: Cameras.post_step over the pre-despawn list runs between step_phys
