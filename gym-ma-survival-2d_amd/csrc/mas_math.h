@@ -43,11 +43,13 @@ MAS_HD float opq(float x) { asm volatile("" : "+v"(x)); return x; }
 MAS_HD int opq(int x) { asm volatile("" : "+v"(x)); return x; }
 MAS_HD uint32_t opq(uint32_t x) { asm volatile("" : "+v"(x)); return x; }
 MAS_HD double opq(double x) { asm volatile("" : "+v"(x)); return x; }
+MAS_HD uint64_t opq(uint64_t x) { asm volatile("" : "+v"(x)); return x; }
 #else
 MAS_HD float opq(float x) { return x; }
 MAS_HD int opq(int x) { return x; }
 MAS_HD uint32_t opq(uint32_t x) { return x; }
 MAS_HD double opq(double x) { return x; }
+MAS_HD uint64_t opq(uint64_t x) { return x; }
 #endif
 MAS_HD V2 opq(V2 v) { return mk(opq(v.x), opq(v.y)); }
 MAS_HD V2 add(V2 a, V2 b) { return mk(a.x + b.x, a.y + b.y); }

@@ -51,17 +51,61 @@ class PPOConfig:
     autocast_bf16: bool = True
 
 
+def _split_k(m: int, cap: int = 64) -> int:
+    c = 1
+    while c < cap and m % (2 * c) == 0 and m // (2 * c) >= 4096:
+        c *= 2
+    return c
+
+
+class _LinearSplitKFn(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient is computed split-K: for a PPO
+    minibatch of millions of rows, dW = dY^T X has a tiny M x N and a huge K,
+    and a single GEMM there launches a handful of tiles; a batched GEMM over
+    row chunks followed by a sum fills the GPU."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        x2 = x.reshape(-1, x.shape[-1])
+        g2 = gy.reshape(-1, gy.shape[-1])
+        gx = (g2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        m = x2.shape[0]
+        c = _split_k(m)
+        gw = torch.bmm(g2.reshape(c, m // c, -1).transpose(1, 2), x2.reshape(c, m // c, -1)).sum(0)
+        gb = g2.reshape(c, m // c, -1).sum(1).sum(0)
+        return gx, gw.to(w.dtype), gb
+
+
+class LinearSplitK(nn.Linear):
+    def forward(self, x):
+        if torch.is_autocast_enabled(x.device.type):
+            dt = torch.get_autocast_dtype(x.device.type)
+            with torch.autocast(x.device.type, enabled=False):
+                return _LinearSplitKFn.apply(x.to(dt), self.weight.to(dt), self.bias.to(dt))
+        return _LinearSplitKFn.apply(x, self.weight, self.bias)
+
+
 class PolicyMLP(nn.Module):
     """Shared across agents: obs [.., D] -> (logits [.., 15], value [..])."""
 
     def __init__(self, obs_dim: int, hidden: int = 256):
         super().__init__()
-        self.body = nn.Sequential(nn.Linear(obs_dim, hidden), nn.Tanh(), nn.Linear(hidden, hidden), nn.Tanh())
-        self.head = nn.Linear(hidden, N_LOGITS + 1)
+        self.body = nn.Sequential(LinearSplitK(obs_dim, hidden), nn.Tanh(), LinearSplitK(hidden, hidden), nn.Tanh())
+        self.head = LinearSplitK(hidden, N_LOGITS + 1)
 
     def forward(self, x):
         h = self.head(self.body(x))
         return h[..., :N_LOGITS].float(), h[..., N_LOGITS].float()
+
+    def forward_raw(self, x):
+        """[.., 16] fp32 head output: 15 logits then the value."""
+        return self.head(self.body(x)).float()
 
 
 def _split_heads(logits):
@@ -78,6 +122,18 @@ def sample_actions(logits, gen: Optional[torch.Generator] = None):
         acts.append(a)
         logp = logp + lsm.gather(-1, a.unsqueeze(-1)).squeeze(-1)
     return torch.stack(acts, dim=-1).to(torch.int8), logp
+
+
+def sample_actions_hip(logits, seed, step, actions_out, logp_out):
+    """HIP sampler (include/masurvival.h mas_sample_actions): logits [M, >=15]
+    fp32 with unit column stride; writes actions_out int8 [M, 6], logp_out [M]."""
+    lib = load_library()
+    M = logits.shape[0]
+    assert logits.is_cuda and logits.dtype == torch.float32 and logits.stride(1) == 1
+    assert actions_out.is_contiguous() and logp_out.is_contiguous()
+    check(lib.mas_sample_actions(M, ctypes.c_void_p(logits.data_ptr()), logits.stride(0), seed, step,
+                                 ctypes.c_void_p(actions_out.data_ptr()), ctypes.c_void_p(logp_out.data_ptr()),
+                                 ctypes.c_void_p(torch.cuda.current_stream(logits.device).cuda_stream)))
 
 
 def evaluate_actions(logits, actions):
@@ -178,19 +234,44 @@ class PPOTrainer:
         self.buf.obs[0].copy_(env.reset())
         self.last_stats = {}
         self.gae_impl = gae  # the HIP kernel; CPU tests inject gae_reference_into
+        self.seed = int(seed) * 1000003 + (dist.get_rank() if dist.is_initialized() else 0)
+        self.steps_taken = 0
+        self._rollout_policy = None
+        self._sync_rollout_policy()
 
     def _fwd(self, x):
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.cfg.autocast_bf16):
             return self.policy(x)
 
     @torch.no_grad()
+    def _sync_rollout_policy(self):
+        """bf16 copy of the policy for the rollout forward (refreshed after each
+        update): no per-step weight casts under autocast."""
+        if self.cfg.autocast_bf16 and self.device.type == 'cuda':
+            if self._rollout_policy is None:
+                import copy
+                self._rollout_policy = copy.deepcopy(self.policy).to(torch.bfloat16)
+            for d, s_ in zip(self._rollout_policy.parameters(), self.policy.parameters()):
+                d.copy_(s_)
+
+    @torch.no_grad()
     def rollout_step(self, t):
         b = self.buf
-        logits, v = self._fwd(b.obs[t])
-        a, lp = sample_actions(logits, self.gen)
-        b.actions[t].copy_(a)
-        b.logp[t].copy_(lp)
-        b.values[t].copy_(v)
+        if self.device.type == 'cuda':
+            if self._rollout_policy is not None:
+                h = self._rollout_policy.forward_raw(b.obs[t].to(torch.bfloat16))  # [N, A, 16] fp32
+            else:
+                h = self.policy.forward_raw(b.obs[t])
+            h2 = h.reshape(-1, N_LOGITS + 1)
+            sample_actions_hip(h2, self.seed, self.steps_taken, b.actions[t].view(-1, 6), b.logp[t].view(-1))
+            b.values[t].copy_(h[..., N_LOGITS])
+        else:  # CPU stand-in tests
+            logits, v = self._fwd(b.obs[t])
+            a, lp = sample_actions(logits, self.gen)
+            b.actions[t].copy_(a)
+            b.logp[t].copy_(lp)
+            b.values[t].copy_(v)
+        self.steps_taken += 1
         self.env.step(b.actions[t], out=(b.obs[t + 1], b.rewards[t], b.dones[t]))
 
     @torch.no_grad()
@@ -233,6 +314,7 @@ class PPOTrainer:
                 nn.utils.clip_grad_norm_(params, c.max_grad_norm)
                 self.opt.step()
         self.last_stats = {'loss': loss.detach(), 'pg': pg.detach(), 'v': vl.detach()}
+        self._sync_rollout_policy()
         b.obs[0].copy_(b.obs[c.horizon])
 
     def iteration(self):

@@ -152,6 +152,15 @@ int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards
             const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
             void* stream);
 
+/* Rollout side: sample the six action heads (MultiDiscrete [3,3,3,2,2,2]) of
+ * n_rows agent rows from logits [n_rows][row_stride] (first 15 floats of a
+ * row: the heads' logits in order), Gumbel-max with a counter-based RNG keyed
+ * by (seed, step, row); writes actions int8 [n_rows][6] and the log-prob of
+ * the drawn actions float [n_rows].  Batched form of the reference's policy
+ * act() (demo.py:14-22).  DEVICE pointers. */
+int mas_sample_actions(int64_t n_rows, const float* logits, int64_t row_stride, uint64_t seed, uint64_t step,
+                       int8_t* actions, float* logp, void* stream);
+
 /* Diagnostics (synchronises the device): host_out[0] = envs of the last
  * mas_step that left the contact-free physics fast path and ran the general
  * physics kernel (contacts, TOI events, box despawns). */

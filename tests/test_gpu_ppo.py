@@ -37,3 +37,30 @@ def test_ppo_iteration_on_env():
         tr.iteration()
     assert torch.isfinite(tr.last_stats['loss'])
     assert bool(torch.isfinite(tr.buf.adv).all()) and bool(torch.isfinite(tr.buf.obs).all())
+
+
+def test_hip_sampler_logp_and_distribution():
+    from masurvival.ppo import evaluate_actions, sample_actions_hip
+    g = torch.Generator(device='cuda').manual_seed(3)
+    M = 200000
+    row = torch.randn((1, 16), device='cuda', generator=g) * 1.5
+    logits = row.repeat(M, 1).contiguous()
+    acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
+    lp = torch.empty((M,), dtype=torch.float32, device='cuda')
+    sample_actions_hip(logits, 1234, 7, acts, lp)
+    ref_lp, _ = evaluate_actions(logits[:, :15], acts)
+    torch.testing.assert_close(lp, ref_lp, atol=1e-5, rtol=1e-5)
+    off = 0
+    for h, n in enumerate((3, 3, 3, 2, 2, 2)):
+        p = torch.softmax(row[0, off:off + n], dim=0)
+        freq = torch.bincount(acts[:, h].long(), minlength=n).float() / M
+        assert int(acts[:, h].max()) < n and int(acts[:, h].min()) >= 0
+        assert torch.allclose(freq, p, atol=0.01), (h, freq, p)
+        off += n
+    # different step -> different draws, same step -> same draws
+    acts2 = torch.empty_like(acts)
+    sample_actions_hip(logits, 1234, 8, acts2, lp)
+    assert not torch.equal(acts, acts2)
+    acts3 = torch.empty_like(acts)
+    sample_actions_hip(logits, 1234, 7, acts3, lp)
+    assert torch.equal(acts, acts3)

@@ -112,3 +112,21 @@ def test_two_rank_gloo_update(tmp_path):
     # while each rank alone is not exactly centred
     assert abs(s1 / n) < 1e-5 and abs(s2 / n - 1) < 1e-3
     assert abs(res[0]['s1'] / res[0]['n']) > 1e-4
+
+
+def test_split_k_linear_matches_nn_linear():
+    from masurvival.ppo import LinearSplitK
+    torch.manual_seed(0)
+    a = torch.nn.Linear(24, 16)
+    b = LinearSplitK(24, 16)
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(8192 * 4, 24, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    ya, yb = a(x), b(x2)
+    torch.testing.assert_close(ya, yb)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(x.grad, x2.grad)
+    torch.testing.assert_close(a.weight.grad, b.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(a.bias.grad, b.bias.grad, rtol=1e-4, atol=1e-3)
