@@ -39,6 +39,17 @@ MAS_DECLARE(ffa)
 #ifdef MAS_HAVE_xl
 MAS_DECLARE(xl)
 #endif
+// fused policy MLP of the PPO consumer (mas_policy.hip)
+int64_t policy_packed_bytes(int D);
+int64_t policy_blocks(int64_t M);
+hipError_t policy_pack(int D, const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                       const float* b3, void* packed, hipStream_t s);
+hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, void* xb, int64_t xb_stride,
+                      uint64_t seed, uint64_t step, int8_t* act, float* logp, float* value, hipStream_t s);
+hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, int64_t xb_stride, const int8_t* act,
+                        const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
+                        float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
+                        float* partials, hipStream_t s);
 }  // namespace mas
 
 namespace {
@@ -635,6 +646,55 @@ int mas_sample_actions(int64_t n_rows, const float* logits, int64_t row_stride, 
     hipLaunchKernelGGL(k_sample, g, dim3(256), 0, (hipStream_t)stream, n_rows, logits, row_stride, seed, step,
                        actions, logp);
     HIP_TRY(hipGetLastError());
+    return MAS_OK;
+}
+
+int64_t mas_policy_packed_bytes(int32_t obs_dim) { return obs_dim > 0 ? policy_packed_bytes(obs_dim) : -1; }
+
+int64_t mas_policy_blocks(int64_t n_rows) { return n_rows > 0 ? policy_blocks(n_rows) : 0; }
+
+int mas_policy_pack(int32_t obs_dim, const float* w1, const float* b1, const float* w2, const float* b2,
+                    const float* w3, const float* b3, void* packed, void* stream)
+{
+    if (obs_dim <= 0 || !w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !packed)
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_pack: bad argument");
+    HIP_TRY(policy_pack(obs_dim, w1, b1, w2, b2, w3, b3, packed, (hipStream_t)stream));
+    return MAS_OK;
+}
+
+static bool policy_x_ok(int32_t obs_dim, int64_t x_stride)
+{
+    return x_stride >= ((obs_dim + 15) / 16) * 16 && x_stride % 8 == 0;
+}
+
+int mas_policy_act(const void* packed, int32_t obs_dim, int64_t n_rows, const float* obs, void* x_bf16,
+                   int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp, float* value,
+                   void* stream)
+{
+    if (!packed || obs_dim <= 0 || n_rows <= 0 || !obs || !actions || !logp || !value)
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_act: bad argument");
+    if (x_bf16 && !policy_x_ok(obs_dim, x_stride))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_act: x_stride must be a multiple of 8 >= 16*ceil(obs_dim/16)");
+    if ((reinterpret_cast<uintptr_t>(obs) & 15) || (reinterpret_cast<uintptr_t>(actions) & 1) ||
+        (x_bf16 && (reinterpret_cast<uintptr_t>(x_bf16) & 15)))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_act: misaligned buffer (obs/x 16 B, actions 2 B)");
+    HIP_TRY(policy_act(packed, obs_dim, n_rows, obs, x_bf16, x_stride, seed, step, actions, logp, value,
+                       (hipStream_t)stream));
+    return MAS_OK;
+}
+
+int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
+                     const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
+                     float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
+                     float* partials, void* stream)
+{
+    if (!packed || obs_dim <= 0 || n_rows <= 0 || !x_bf16 || !actions || !old_logp || !adv || !ret || !h1 || !h2 ||
+        !da1 || !da2 || !dz || !partials)
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_train: bad argument");
+    if (!policy_x_ok(obs_dim, x_stride) || (reinterpret_cast<uintptr_t>(x_bf16) & 15))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_train: x must be 16-B aligned with a padded row stride");
+    HIP_TRY(policy_train(packed, obs_dim, n_rows, x_bf16, x_stride, actions, old_logp, adv, ret, clip, vf_coef,
+                         ent_coef, scale, h1, h2, da1, da2, dz, partials, (hipStream_t)stream));
     return MAS_OK;
 }
 

@@ -1,0 +1,531 @@
+// mas_policy.hip -- the PPO consumer's shared-parameter policy MLP as fused
+// gfx950 kernels (the reference ships no trainer).
+//
+//   obs [M][D] -> z1 = W1 x + b1 -> h1 = tanh(z1) (256)
+//              -> z2 = W2 h1 + b2 -> h2 = tanh(z2) (256)
+//              -> z3 = W3 h2 + b3 (16: the six heads' 15 logits, then the value)
+//
+// Everything is computed TRANSPOSED, features x rows: one wave owns 32 agent
+// rows, which sit on the lanes (the column of every 32x32 MFMA tile), and the
+// features sit in the registers.  The f32 result of one
+// v_mfma_f32_32x32x16_bf16 is then, converted to bf16 in place, the B
+// operand of the next layer's MFMA (a product that sums over the tile's ROW
+// index needs no lane movement and no LDS; cdna_hip_programming.md section 3):
+// the only price is a permuted k order inside every 16-deep k-step, which the
+// host-side packing (k_pack) folds into the weights once per update.  Layer 3
+// pads W3 to 32 rows and puts the 16 real outputs on the rows that lane half 0
+// holds, so lanes 0..31 end with their agent row's 16 outputs in registers.
+//
+// Weights are read as pre-packed 1-KiB fragments (one 16-B load per lane per
+// MFMA, fully coalesced) from the L2-resident packed image; x is read once.
+//
+// k_policy_act   rollout: forward + Gumbel-max sampling of the six heads (the
+//                exact RNG of k_sample) -> actions, log-prob, value; also
+//                writes the bf16 copy of x the update reads.
+// k_policy_train update: forward, the PPO loss gradient per row
+//                (clipped surrogate + value MSE - entropy bonus), and the
+//                backward data path dz -> dA2 -> dA1 in the same registers;
+//                writes h1, h2, dA1, dA2, dz feature-major ([F][M] bf16) for
+//                the weight-gradient GEMMs and per-block loss partials.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mas {
+namespace pol {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int kH = 256;   // hidden width
+constexpr int kMT = 8;    // 32-row M-tiles of a hidden layer
+constexpr int kO = 16;    // real outputs of layer 3 (15 logits + value)
+constexpr int kWaves = 4; // waves per workgroup (one per SIMD)
+
+// packed image, in 16-B fragments (bf8), then f32 biases
+struct Layout {
+    int ks1;  // 16-deep k-steps of layer 1 (ceil(D / 16))
+    __host__ __device__ int64_t w1() const { return 0; }                                  // [ks1][8][64]
+    __host__ __device__ int64_t w2() const { return w1() + (int64_t)ks1 * kMT * 64; }     // [8][16][64]
+    __host__ __device__ int64_t w3() const { return w2() + (int64_t)kMT * 16 * 64; }      // [16][64]
+    __host__ __device__ int64_t w3t() const { return w3() + 16 * 64; }                    // [8][2][64]
+    __host__ __device__ int64_t w2t() const { return w3t() + (int64_t)kMT * 2 * 64; }     // [8][16][64]
+    __host__ __device__ int64_t nfrag() const { return w2t() + (int64_t)kMT * 16 * 64; }
+    // biases (floats) after the fragments: b1p [8][2][16], b2p [8][2][16], b3 [16]
+    __host__ __device__ int64_t b1() const { return nfrag() * 4; }
+    __host__ __device__ int64_t b2() const { return b1() + kMT * 2 * 16; }
+    __host__ __device__ int64_t b3() const { return b2() + kMT * 2 * 16; }
+    __host__ __device__ int64_t bytes() const { return (b3() + kO) * 4; }
+};
+
+// row of the 32x32 C tile held in register i by lane half h
+__host__ __device__ inline int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+// row of X carried by element j of lane half h in k-step s of an
+// accumulator-as-operand fragment (registers 8s..8s+7)
+__host__ __device__ inline int prow(int s, int h, int j) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
+// padded layer-3 row of real output o (lane half 0, register o)
+__host__ __device__ inline int orow(int o) { return (o & 3) + 8 * (o >> 2); }
+
+// One thread per packed element: bf16 fragments and permuted f32 biases from
+// the torch fp32 parameters (W1 [256][D], W2 [256][256], W3 [16][256]).
+__global__ void k_pack(int D, int ks1, const float* __restrict__ W1, const float* __restrict__ b1,
+                       const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ W3,
+                       const float* __restrict__ b3, uint8_t* __restrict__ out)
+{
+    const Layout L{ks1};
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __bf16* frag = reinterpret_cast<__bf16*>(out);
+    float* fb = reinterpret_cast<float*>(out);
+    const int64_t nel = L.nfrag() * 8;
+    if (t < nel) {
+        const int64_t f = t >> 3;
+        const int j = (int)(t & 7);
+        const int l = (int)(f & 63), r = l & 31, h = l >> 5;
+        const int64_t g = f >> 6;  // fragment index
+        float v = 0.0f;
+        if (f < L.w2()) {  // W1: g = ks * 8 + mt, natural k order
+            const int ks = (int)(g / kMT), mt = (int)(g % kMT);
+            const int k = 16 * ks + 8 * h + j;
+            v = k < D ? W1[(int64_t)(32 * mt + r) * D + k] : 0.0f;
+        } else if (f < L.w3()) {  // W2: g = mo * 16 + kk (kk = 2 mt + s)
+            const int64_t q = g - L.w2() / 64;
+            const int mo = (int)(q / 16), kk = (int)(q % 16);
+            v = W2[(32 * mo + r) * kH + 32 * (kk >> 1) + prow(kk & 1, h, j)];
+        } else if (f < L.w3t()) {  // W3 (padded to 32 rows): g = kk
+            const int kk = (int)(g - L.w3() / 64);
+            int o = -1;
+            for (int q = 0; q < kO; ++q)
+                if (orow(q) == r) o = q;
+            v = o >= 0 ? W3[o * kH + 32 * (kk >> 1) + prow(kk & 1, h, j)] : 0.0f;
+        } else if (f < L.w2t()) {  // W3pad^T: g = mo * 2 + s
+            const int64_t q = g - L.w3t() / 64;
+            const int mo = (int)(q / 2), s = (int)(q % 2);
+            const int pr = prow(s, h, j);  // padded output row
+            int o = -1;
+            for (int q2 = 0; q2 < kO; ++q2)
+                if (orow(q2) == pr) o = q2;
+            v = o >= 0 ? W3[o * kH + 32 * mo + r] : 0.0f;
+        } else {  // W2^T: g = mt * 16 + kk (kk = 2 mo + s)
+            const int64_t q = g - L.w2t() / 64;
+            const int mt = (int)(q / 16), kk = (int)(q % 16);
+            v = W2[(32 * (kk >> 1) + prow(kk & 1, h, j)) * kH + 32 * mt + r];
+        }
+        frag[t] = (__bf16)v;
+        return;
+    }
+    const int64_t u = t - nel;  // biases
+    if (u < 2 * kMT * 2 * 16) {
+        const int which = (int)(u / (kMT * 2 * 16));
+        const int rem = (int)(u % (kMT * 2 * 16));
+        const int mt = rem / 32, h = (rem / 16) & 1, i = rem & 15;
+        const float* b = which == 0 ? b1 : b2;
+        fb[(which == 0 ? L.b1() : L.b2()) + rem] = b[32 * mt + crow(i, h)];
+    } else if (u < 2 * kMT * 2 * 16 + kO) {
+        const int o = (int)(u - 2 * kMT * 2 * 16);
+        fb[L.b3() + o] = b3[o];
+    }
+}
+
+__device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c)
+{
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float tanh_fast(float x)
+{
+    x = fminf(fmaxf(x, -15.0f), 15.0f);
+    const float e = __expf(2.0f * x);
+    return __fdividef(e - 1.0f, e + 1.0f);
+}
+
+__device__ __forceinline__ void load16(const float* __restrict__ p, float* v)
+{
+    const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 a = q[k];
+        v[4 * k] = a.x;
+        v[4 * k + 1] = a.y;
+        v[4 * k + 2] = a.z;
+        v[4 * k + 3] = a.w;
+    }
+}
+
+// x fragment of k-step ks for this lane's row from fp32 obs [M][D]
+__device__ __forceinline__ bf8 x_frag_f32(const float* __restrict__ obs, int64_t row, bool ok, int D, int k0)
+{
+    bf8 f;
+    const float* p = obs + row * D + k0;
+    if (ok && (D & 3) == 0 && k0 + 8 <= D) {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        f[0] = (__bf16)a.x; f[1] = (__bf16)a.y; f[2] = (__bf16)a.z; f[3] = (__bf16)a.w;
+        f[4] = (__bf16)b.x; f[5] = (__bf16)b.y; f[6] = (__bf16)b.z; f[7] = (__bf16)b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (__bf16)((ok && k0 + j < D) ? p[j] : 0.0f);
+    }
+    return f;
+}
+
+// layer 1 over all k-steps into 8 M-tile accumulators, then bias + tanh into
+// the bf16 operand fragments h1[mt][s]
+template <class XF>
+__device__ __forceinline__ void layer1(const bf8* __restrict__ W, const float* __restrict__ b1p, int ks1, int l, XF xf,
+                                       bf8 (&h1)[kMT][2])
+{
+    const int h = l >> 5;
+    f16v acc[kMT];
+#pragma unroll
+    for (int mt = 0; mt < kMT; ++mt) acc[mt] = f16v{};
+#pragma unroll 2
+    for (int ks = 0; ks < ks1; ++ks) {
+        const bf8 x = xf(ks);
+        const bf8* w = W + (int64_t)ks * kMT * 64 + l;
+#pragma unroll
+        for (int mt = 0; mt < kMT; ++mt) acc[mt] = mfma(w[mt * 64], x, acc[mt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < kMT; ++mt) {
+        float b[16];
+        load16(b1p + (mt * 2 + h) * 16, b);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h1[mt][i >> 3][i & 7] = (__bf16)tanh_fast(acc[mt][i] + b[i]);
+    }
+}
+
+// layer 2 (by output M-tile) fused with layer 3; h2 kept when KEEP
+template <bool KEEP>
+__device__ __forceinline__ f16v layers23(const bf8* __restrict__ W2, const bf8* __restrict__ W3,
+                                         const float* __restrict__ b2p, int l, const bf8 (&h1)[kMT][2],
+                                         bf8 (&h2)[kMT][2])
+{
+    const int h = l >> 5;
+    f16v z3 = f16v{};
+#pragma unroll
+    for (int mo = 0; mo < kMT; ++mo) {
+        f16v a = f16v{};
+        const bf8* w = W2 + (int64_t)mo * 16 * 64 + l;
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) a = mfma(w[kk * 64], h1[kk >> 1][kk & 1], a);
+        float b[16];
+        load16(b2p + (mo * 2 + h) * 16, b);
+        bf8 f[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) f[i >> 3][i & 7] = (__bf16)tanh_fast(a[i] + b[i]);
+        z3 = mfma(W3[(2 * mo) * 64 + l], f[0], z3);
+        z3 = mfma(W3[(2 * mo + 1) * 64 + l], f[1], z3);
+        if (KEEP) {
+            h2[mo][0] = f[0];
+            h2[mo][1] = f[1];
+        }
+    }
+    return z3;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+constexpr int kHeadN[6] = {3, 3, 3, 2, 2, 2};
+constexpr int kHeadOff[6] = {0, 3, 6, 9, 11, 13};
+
+__global__ __launch_bounds__(64 * kWaves) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
+                                                             int64_t M, const float* __restrict__ obs,
+                                                             __bf16* __restrict__ xb, int64_t xb_stride,
+                                                             uint64_t seed, uint64_t step, int8_t* __restrict__ act,
+                                                             float* __restrict__ logp, float* __restrict__ value)
+{
+    const Layout Lo{ks1};
+    const bf8* F = reinterpret_cast<const bf8*>(packed);
+    const float* FB = reinterpret_cast<const float*>(packed);
+    const int l = threadIdx.x & 63, h = l >> 5;
+    const int64_t row0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32;
+    if (row0 >= M) return;  // wave-uniform
+    const int64_t row = row0 + (l & 31);
+    const bool ok = row < M;
+    bf8 h1[kMT][2], h2[kMT][2];
+    layer1(F + Lo.w1(), FB + Lo.b1(), ks1, l,
+           [&](int ks) {
+               const bf8 x = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
+               if (xb != nullptr && ok) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x;
+               return x;
+           },
+           h1);
+    const f16v z3 = layers23<false>(F + Lo.w2(), F + Lo.w3(), FB + Lo.b2(), l, h1, h2);
+    if (h != 0 || !ok) return;
+    float z[kO];
+    const float* b3 = FB + Lo.b3();
+#pragma unroll
+    for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
+    // Gumbel-max over each head; the RNG stream of k_sample (mas_capi.hip)
+    const uint64_t base = mix64(seed ^ mix64(step * 0x100000001B3ULL + (uint64_t)row));
+    float lp = 0.0f;
+    uint32_t packed_a[2] = {0u, 0u};
+#pragma unroll
+    for (int hd = 0; hd < 6; ++hd) {
+        const int n = kHeadN[hd], off = kHeadOff[hd];
+        float mx = z[off];
+#pragma unroll
+        for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
+        float se = 0.0f;
+#pragma unroll
+        for (int k = 0; k < n; ++k) se += expf(z[off + k] - mx);
+        const float lse = mx + logf(se);
+        int best = 0;
+        float bv = -INFINITY, lb = z[off];
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+            const uint64_t r = mix64(base + (uint64_t)(hd * 4 + k));
+            const float u = ((float)(r >> 40) + 0.5f) * (1.0f / 16777216.0f);
+            const float g = z[off + k] - logf(-logf(u));
+            if (g > bv) {
+                bv = g;
+                best = k;
+                lb = z[off + k];
+            }
+        }
+        lp += lb - lse;
+        packed_a[hd >> 2] |= (uint32_t)best << (8 * (hd & 3));
+    }
+    // 6 int8 per row (2-B aligned): three 2-B stores
+    uint16_t* ap = reinterpret_cast<uint16_t*>(act + row * 6);
+    ap[0] = (uint16_t)packed_a[0];
+    ap[1] = (uint16_t)(packed_a[0] >> 16);
+    ap[2] = (uint16_t)packed_a[1];
+    logp[row] = lp;
+    value[row] = z[kO - 1];
+}
+
+struct TrainArgs {
+    const uint8_t* packed;
+    int ks1;
+    int64_t M;              // rows of this minibatch
+    const __bf16* xb;       // [M][xb_stride] bf16
+    int64_t xb_stride;
+    const int8_t* act;      // [M][6]
+    const float* old_logp;  // [M]
+    const float* adv;       // [M] (normalised)
+    const float* ret;       // [M]
+    float clip, vf_coef, ent_coef, scale;  // scale = 1 / rows of the minibatch
+    __bf16 *h1, *h2, *da1, *da2, *dz;      // feature-major [256 | 16][M]
+    float* partials;        // [gridDim.x][4]: sum pg, sum (v-ret)^2, sum entropy, clipped count
+};
+
+__global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
+{
+    __shared__ float red[kWaves][4];
+    const Layout Lo{A.ks1};
+    const bf8* F = reinterpret_cast<const bf8*>(A.packed);
+    const float* FB = reinterpret_cast<const float*>(A.packed);
+    const int l = threadIdx.x & 63, h = l >> 5, wv = threadIdx.x >> 6;
+    const int64_t M = A.M;
+    const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wv) * 32;
+    const int64_t row = row0 + (l & 31);
+    const bool ok = row < M;
+    float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (row0 < M) {  // wave-uniform
+        bf8 h1[kMT][2], h2[kMT][2];
+        layer1(F + Lo.w1(), FB + Lo.b1(), A.ks1, l,
+               [&](int ks) {
+                   bf8 x;
+                   if (ok) {
+                       x = *reinterpret_cast<const bf8*>(A.xb + row * A.xb_stride + 16 * ks + 8 * h);
+                   } else {
+#pragma unroll
+                       for (int j = 0; j < 8; ++j) x[j] = (__bf16)0.0f;
+                   }
+                   return x;
+               },
+               h1);
+        const f16v z3 = layers23<true>(F + Lo.w2(), F + Lo.w3(), FB + Lo.b2(), l, h1, h2);
+        // feature-major activations for the weight gradients
+        if (ok) {
+#pragma unroll
+            for (int mt = 0; mt < kMT; ++mt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t f = 32 * mt + crow(i, h);
+                    A.h1[f * M + row] = h1[mt][i >> 3][i & 7];
+                    A.h2[f * M + row] = h2[mt][i >> 3][i & 7];
+                }
+        }
+        // PPO loss gradient of this row (lane half 0 holds the 16 outputs)
+        float dz[kO];
+#pragma unroll
+        for (int o = 0; o < kO; ++o) dz[o] = 0.0f;
+        if (h == 0 && ok) {
+            float z[kO];
+            const float* b3 = FB + Lo.b3();
+#pragma unroll
+            for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
+            const int8_t* a = A.act + row * 6;
+            float lsm[15], p[15], hent[6];
+            float lp = 0.0f, ent = 0.0f;
+#pragma unroll
+            for (int hd = 0; hd < 6; ++hd) {
+                const int n = kHeadN[hd], off = kHeadOff[hd];
+                float mx = z[off];
+#pragma unroll
+                for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
+                float se = 0.0f;
+#pragma unroll
+                for (int k = 0; k < n; ++k) se += expf(z[off + k] - mx);
+                const float lse = mx + logf(se);
+                float e = 0.0f;
+                const int ak = a[hd];
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    lsm[off + k] = z[off + k] - lse;
+                    p[off + k] = expf(lsm[off + k]);
+                    e -= p[off + k] * lsm[off + k];
+                    if (k == ak) lp += lsm[off + k];
+                }
+                hent[hd] = e;
+                ent += e;
+            }
+            const float adv = A.adv[row];
+            const float ratio = expf(lp - A.old_logp[row]);
+            const float s1 = ratio * adv;
+            const float rc = fminf(fmaxf(ratio, 1.0f - A.clip), 1.0f + A.clip);
+            const float s2 = rc * adv;
+            // d(-min(s1, s2))/d lp: the surrogate is differentiable through
+            // s1 where it is the minimum (ties included: then s1 == s2 with
+            // the ratio inside the clip range)
+            const float glp = s1 <= s2 ? -s1 : 0.0f;
+            const float sc = A.scale;
+#pragma unroll
+            for (int hd = 0; hd < 6; ++hd) {
+                const int n = kHeadN[hd], off = kHeadOff[hd];
+                const int ak = a[hd];
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    const float oh = k == ak ? 1.0f : 0.0f;
+                    dz[off + k] = sc * (glp * (oh - p[off + k]) + A.ent_coef * p[off + k] * (lsm[off + k] + hent[hd]));
+                }
+            }
+            const float dv = z[kO - 1] - A.ret[row];
+            dz[kO - 1] = sc * A.vf_coef * 2.0f * dv;
+            st[0] = -fminf(s1, s2);
+            st[1] = dv * dv;
+            st[2] = ent;
+            st[3] = fabsf(ratio - 1.0f) > A.clip ? 1.0f : 0.0f;
+#pragma unroll
+            for (int o = 0; o < kO; ++o) A.dz[(int64_t)o * M + row] = (__bf16)dz[o];
+        }
+        bf8 dzf[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dzf[i >> 3][i & 7] = (__bf16)dz[i];
+        // dA2 = (W3^T dz) * (1 - h2^2), by M-tile of layer 2
+        bf8 da2[kMT][2];
+        const bf8* W3T = F + Lo.w3t() + l;
+#pragma unroll
+        for (int mo = 0; mo < kMT; ++mo) {
+            f16v g = f16v{};
+            g = mfma(W3T[(mo * 2) * 64], dzf[0], g);
+            g = mfma(W3T[(mo * 2 + 1) * 64], dzf[1], g);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float hv = (float)h2[mo][i >> 3][i & 7];
+                da2[mo][i >> 3][i & 7] = (__bf16)(g[i] * (1.0f - hv * hv));
+            }
+            if (ok) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) A.da2[(int64_t)(32 * mo + crow(i, h)) * M + row] = da2[mo][i >> 3][i & 7];
+            }
+        }
+        // dA1 = (W2^T dA2) * (1 - h1^2), by M-tile of layer 1
+        const bf8* W2T = F + Lo.w2t() + l;
+#pragma unroll
+        for (int mt = 0; mt < kMT; ++mt) {
+            f16v g = f16v{};
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) g = mfma(W2T[(mt * 16 + kk) * 64], da2[kk >> 1][kk & 1], g);
+            if (ok) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float hv = (float)h1[mt][i >> 3][i & 7];
+                    A.da1[(int64_t)(32 * mt + crow(i, h)) * M + row] = (__bf16)(g[i] * (1.0f - hv * hv));
+                }
+            }
+        }
+    }
+    // per-block loss partials
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float v = st[k];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (l == 0) red[wv][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v += red[w][threadIdx.x];
+        A.partials[(int64_t)blockIdx.x * 4 + threadIdx.x] = v;
+    }
+}
+
+}  // namespace pol
+
+// ---------------------------------------------------------------------------
+// launchers (argument checks are in the C-ABI wrappers, mas_capi.hip)
+// ---------------------------------------------------------------------------
+int64_t policy_packed_bytes(int D) { return pol::Layout{(D + 15) / 16}.bytes(); }
+
+hipError_t policy_pack(int D, const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                       const float* b3, void* packed, hipStream_t s)
+{
+    const pol::Layout L{(D + 15) / 16};
+    const int64_t n = L.nfrag() * 8 + 2 * pol::kMT * 2 * 16 + pol::kO;
+    hipLaunchKernelGGL(pol::k_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, D, L.ks1, W1, b1, W2, b2, W3,
+                       b3, (uint8_t*)packed);
+    return hipGetLastError();
+}
+
+int64_t policy_blocks(int64_t M) { return (M + 32 * pol::kWaves - 1) / (32 * pol::kWaves); }
+
+hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, void* xb, int64_t xb_stride,
+                      uint64_t seed, uint64_t step, int8_t* act, float* logp, float* value, hipStream_t s)
+{
+    hipLaunchKernelGGL(pol::k_policy_act, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s,
+                       (const uint8_t*)packed, D, (D + 15) / 16, M, obs, (__bf16*)xb, xb_stride, seed, step, act,
+                       logp, value);
+    return hipGetLastError();
+}
+
+hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, int64_t xb_stride, const int8_t* act,
+                        const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
+                        float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
+                        float* partials, hipStream_t s)
+{
+    pol::TrainArgs A;
+    A.packed = (const uint8_t*)packed;
+    A.ks1 = (D + 15) / 16;
+    A.M = M;
+    A.xb = (const __bf16*)xb;
+    A.xb_stride = xb_stride;
+    A.act = act;
+    A.old_logp = old_logp;
+    A.adv = adv;
+    A.ret = ret;
+    A.clip = clip;
+    A.vf_coef = vf_coef;
+    A.ent_coef = ent_coef;
+    A.scale = scale;
+    A.h1 = (__bf16*)h1;
+    A.h2 = (__bf16*)h2;
+    A.da1 = (__bf16*)da1;
+    A.da2 = (__bf16*)da2;
+    A.dz = (__bf16*)dz;
+    A.partials = partials;
+    hipLaunchKernelGGL(pol::k_policy_train, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, A);
+    return hipGetLastError();
+}
+
+}  // namespace mas

@@ -63,6 +63,14 @@ SIGNATURES = {
     'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_sample_actions': (c_int32, [c_int64, c_void_p, c_int64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p,
                                      c_void_p]),
+    'mas_policy_packed_bytes': (c_int64, [c_int32]),
+    'mas_policy_blocks': (c_int64, [c_int64]),
+    'mas_policy_pack': (c_int32, [c_int32] + [c_void_p] * 8),
+    'mas_policy_act': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_void_p, c_int64, ctypes.c_uint64,
+                                 ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'mas_policy_train': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+                         + [c_void_p] * 7),
     'mas_last_error': (c_char_p, []),
     'mas_abi_version': (c_int32, []),
 }

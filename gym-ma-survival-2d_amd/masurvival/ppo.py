@@ -49,6 +49,9 @@ class PPOConfig:
     ent_coef: float = 0.01
     max_grad_norm: float = 0.5
     autocast_bf16: bool = True
+    # fused HIP policy kernels (mas_policy_act / mas_policy_train): default on
+    # a GPU when hidden == 256; the torch path stays as the CPU / reference path
+    fused: Optional[bool] = None
 
 
 def _split_k(m: int, cap: int = 64) -> int:
@@ -188,6 +191,115 @@ def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sum
     sums_out[1] = (adv.double() ** 2).sum()
 
 
+def _splitk_nt(a, b):
+    """a [F, K] @ b[G, K]^T in fp32 for a huge K, as a batched GEMM over K
+    chunks (bf16 in, partial sums reduced in fp32)."""
+    F_, K = a.shape
+    G = b.shape[0]
+    c = _split_k(K)
+    pa = a.view(F_, c, K // c).permute(1, 0, 2)
+    pb = b.view(G, c, K // c).permute(1, 2, 0)
+    return torch.bmm(pa, pb).sum(0, dtype=torch.float32)
+
+
+def _splitk_nn(a, x):
+    """a [F, K] @ x [K, G] in fp32 for a huge K (x row-major, any row stride)."""
+    F_, K = a.shape
+    c = _split_k(K)
+    pa = a.view(F_, c, K // c).permute(1, 0, 2)
+    px = x.reshape(c, K // c, x.shape[1]) if x.is_contiguous() else x.unflatten(0, (c, K // c))
+    return torch.bmm(pa, px).sum(0, dtype=torch.float32)
+
+
+class FusedPolicy:
+    """The HIP policy kernels (include/masurvival.h mas_policy_*) over a
+    PolicyMLP's fp32 parameters: ``pack()`` after every optimizer step, ``act``
+    for the rollout, ``grads`` for one PPO minibatch.  Hidden width 256."""
+
+    def __init__(self, policy: 'PolicyMLP', obs_dim: int, device):
+        self.lib = load_library()
+        self.policy, self.D, self.device = policy, int(obs_dim), device
+        self.Dp = 16 * ((self.D + 15) // 16)
+        w1, w2 = policy.body[0].weight, policy.body[2].weight
+        assert w1.shape == (256, self.D) and w2.shape == (256, 256) and policy.head.weight.shape == (16, 256)
+        self.packed = torch.empty((int(self.lib.mas_policy_packed_bytes(self.D)),), dtype=torch.uint8, device=device)
+        self._bufs = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @torch.no_grad()
+    def pack(self):
+        p = self.policy
+        ts = [p.body[0].weight, p.body[0].bias, p.body[2].weight, p.body[2].bias, p.head.weight, p.head.bias]
+        ts = [t.detach().float().contiguous() for t in ts]
+        check(self.lib.mas_policy_pack(self.D, *[ctypes.c_void_p(t.data_ptr()) for t in ts],
+                                       ctypes.c_void_p(self.packed.data_ptr()), self._stream()))
+
+    @torch.no_grad()
+    def act(self, obs, seed, step, actions, logp, value, xb=None):
+        """obs [M, D] fp32 rows -> actions int8 [M, 6], logp, value [M];
+        xb [M, Dp] bf16 (optional) receives the rows as the update reads them."""
+        M = obs.shape[0]
+        assert obs.is_contiguous() and obs.dtype == torch.float32 and obs.shape[1] == self.D
+        assert actions.is_contiguous() and logp.is_contiguous() and value.is_contiguous()
+        xp = ctypes.c_void_p(xb.data_ptr()) if xb is not None else None
+        check(self.lib.mas_policy_act(ctypes.c_void_p(self.packed.data_ptr()), self.D, M, ctypes.c_void_p(obs.data_ptr()),
+                                      xp, self.Dp, int(seed), int(step), ctypes.c_void_p(actions.data_ptr()),
+                                      ctypes.c_void_p(logp.data_ptr()), ctypes.c_void_p(value.data_ptr()),
+                                      self._stream()))
+
+    def _buffers(self, M):
+        if self._bufs is None or self._bufs['M'] != M:
+            bf = dict(dtype=torch.bfloat16, device=self.device)
+            nb = int(self.lib.mas_policy_blocks(M))
+            self._bufs = {'M': M, 'h1': torch.empty((256, M), **bf), 'h2': torch.empty((256, M), **bf),
+                          'da1': torch.empty((256, M), **bf), 'da2': torch.empty((256, M), **bf),
+                          'dz': torch.empty((16, M), **bf),
+                          'part': torch.empty((nb, 4), dtype=torch.float32, device=self.device)}
+        return self._bufs
+
+    def grads(self, xb, actions, old_logp, adv, ret, cfg: 'PPOConfig'):
+        """Sets .grad of the policy parameters to the gradient of the PPO loss
+        (mean over the M rows) and returns (loss, pg, v, entropy, clipfrac)."""
+        M = xb.shape[0]
+        assert xb.dtype == torch.bfloat16 and xb.shape[1] == self.Dp and xb.is_contiguous()
+        for t in (actions, old_logp, adv, ret):
+            assert t.is_contiguous()
+        B = self._buffers(M)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        check(self.lib.mas_policy_train(ptr(self.packed), self.D, M, ptr(xb), self.Dp, ptr(actions), ptr(old_logp),
+                                        ptr(adv), ptr(ret), cfg.clip, cfg.vf_coef, cfg.ent_coef, 1.0 / M, ptr(B['h1']),
+                                        ptr(B['h2']), ptr(B['da1']), ptr(B['da2']), ptr(B['dz']), ptr(B['part']),
+                                        self._stream()))
+        p = self.policy
+        l1, l2, l3 = p.body[0], p.body[2], p.head
+        grads = {
+            l3.weight: _splitk_nt(B['dz'], B['h2']), l3.bias: B['dz'].sum(1, dtype=torch.float32),
+            l2.weight: _splitk_nt(B['da2'], B['h1']), l2.bias: B['da2'].sum(1, dtype=torch.float32),
+            l1.weight: _splitk_nn(B['da1'], xb)[:, :self.D], l1.bias: B['da1'].sum(1, dtype=torch.float32),
+        }
+        for prm, g in grads.items():
+            if prm.grad is None:
+                prm.grad = g.to(prm.dtype).contiguous()
+            else:
+                prm.grad.copy_(g)
+        s = B['part'].sum(0) / M
+        pg, v, ent, clipfrac = s[0], s[1], s[2], s[3]
+        return pg + cfg.vf_coef * v - cfg.ent_coef * ent, pg, v, ent, clipfrac
+
+
+def policy_loss_reference(policy, x, actions, old_logp, adv, ret, cfg: 'PPOConfig'):
+    """Plain torch fp32 restatement of the PPO loss the fused kernels
+    differentiate (the numerics tests' reference): x fp32 rows [M, D]."""
+    logits, v = policy(x)
+    lp, ent = evaluate_actions(logits, actions)
+    ratio = torch.exp(lp - old_logp)
+    pg = -torch.min(ratio * adv, ratio.clamp(1 - cfg.clip, 1 + cfg.clip) * adv).mean()
+    vl = F.mse_loss(v, ret)
+    return pg + cfg.vf_coef * vl - cfg.ent_coef * ent.mean(), pg, vl, ent.mean()
+
+
 class RolloutBuffer:
     def __init__(self, T, N, A, D, device):
         self.T, self.N, self.A, self.D = T, N, A, D
@@ -201,6 +313,7 @@ class RolloutBuffer:
         self.adv = torch.zeros((T, N, A), **f)
         self.ret = torch.zeros((T, N, A), **f)
         self.adv_sums = torch.zeros((2,), device=device, dtype=torch.float64)
+        self.xb = None  # fused path: bf16 policy-input rows [T, N*A, Dp] written by mas_policy_act
 
 
 def _allreduce_grads(params, world, group=None):
@@ -218,7 +331,16 @@ def _allreduce_grads(params, world, group=None):
 
 
 class PPOTrainer:
-    """Collect T steps of every env on this rank, GAE on device, PPO update."""
+    """Collect T steps of every env on this rank, GAE on device, PPO update.
+
+    Fused path (GPU, hidden 256, the default there): the rollout step is ONE
+    HIP kernel (mas_policy_act: MLP forward + sampling, also storing the bf16
+    policy input for the update); each PPO minibatch is one HIP kernel
+    (mas_policy_train: forward, loss gradient, backward data path) plus three
+    split-K weight-gradient GEMMs.  Minibatches are contiguous time chunks of
+    the rollout (T/minibatches steps of every env), visited in a random order
+    each epoch: no row gather.  The torch path (random row minibatches,
+    autograd) serves the CPU tests and is the numerics reference."""
 
     def __init__(self, env, cfg: PPOConfig = PPOConfig(), seed: int = 0, group=None):
         self.env, self.cfg = env, cfg
@@ -237,7 +359,20 @@ class PPOTrainer:
         self.seed = int(seed) * 1000003 + (dist.get_rank() if dist.is_initialized() else 0)
         self.steps_taken = 0
         self._rollout_policy = None
-        self._sync_rollout_policy()
+        fused = cfg.fused
+        if fused is None:
+            fused = self.device.type == 'cuda' and cfg.hidden == 256
+        self.fused = None
+        if fused:
+            self.fused = FusedPolicy(self.policy, env.obs_dim, self.device)
+            b = self.buf
+            self.buf.xb = torch.zeros((b.T, b.N * b.A, self.fused.Dp), dtype=torch.bfloat16, device=self.device)
+            M = b.N * b.A
+            self._boot = (torch.empty((M, 6), dtype=torch.int8, device=self.device),
+                          torch.empty((M,), dtype=torch.float32, device=self.device))
+            self.fused.pack()
+        else:
+            self._sync_rollout_policy()
 
     def _fwd(self, x):
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.cfg.autocast_bf16):
@@ -257,7 +392,10 @@ class PPOTrainer:
     @torch.no_grad()
     def rollout_step(self, t):
         b = self.buf
-        if self.device.type == 'cuda':
+        if self.fused is not None:
+            self.fused.act(b.obs[t].view(-1, b.D), self.seed, self.steps_taken, b.actions[t].view(-1, 6),
+                           b.logp[t].view(-1), b.values[t].view(-1), xb=b.xb[t])
+        elif self.device.type == 'cuda':
             if self._rollout_policy is not None:
                 h = self._rollout_policy.forward_raw(b.obs[t].to(torch.bfloat16))  # [N, A, 16] fp32
             else:
@@ -277,8 +415,12 @@ class PPOTrainer:
     @torch.no_grad()
     def finish_rollout(self):
         b, c = self.buf, self.cfg
-        _, v = self._fwd(b.obs[c.horizon])
-        b.values[c.horizon].copy_(v)
+        if self.fused is not None:
+            self.fused.act(b.obs[c.horizon].view(-1, b.D), self.seed, 0, self._boot[0], self._boot[1],
+                           b.values[c.horizon].view(-1))
+        else:
+            _, v = self._fwd(b.obs[c.horizon])
+            b.values[c.horizon].copy_(v)
         self.gae_impl(b.rewards, b.values, b.dones, c.gamma, c.lam, b.adv, b.ret, b.adv_sums, self.env.n_agents)
         stats = torch.cat([b.adv_sums, torch.tensor([float(b.adv.numel())], device=self.device,
                                                      dtype=torch.float64)])
@@ -288,7 +430,31 @@ class PPOTrainer:
         var = (stats[1] / stats[2] - mean * mean).clamp_min(0.0)
         b.adv.sub_(mean.float()).div_(var.sqrt().float() + 1e-8)
 
+    def _update_fused(self):
+        b, c = self.buf, self.cfg
+        assert c.horizon % c.minibatches == 0, 'fused update: horizon must split into whole time chunks'
+        tc = c.horizon // c.minibatches
+        params = list(self.policy.parameters())
+        for _ in range(c.epochs):
+            order = torch.randperm(c.minibatches, generator=torch.Generator().manual_seed(self.steps_taken))
+            for k in order.tolist():
+                sl = slice(k * tc, (k + 1) * tc)
+                xb = b.xb[sl].reshape(-1, self.fused.Dp)
+                M = xb.shape[0]
+                loss, pg, vl, ent, cf = self.fused.grads(xb, b.actions[sl].reshape(M, 6), b.logp[sl].reshape(M),
+                                                         b.adv[sl].reshape(M), b.ret[sl].reshape(M), c)
+                if self.world > 1:
+                    _allreduce_grads(params, self.world, self.group)
+                nn.utils.clip_grad_norm_(params, c.max_grad_norm)
+                self.opt.step()
+                self.fused.pack()
+        self.last_stats = {'loss': loss.detach(), 'pg': pg.detach(), 'v': vl.detach(), 'entropy': ent.detach(),
+                           'clipfrac': cf.detach()}
+        b.obs[0].copy_(b.obs[c.horizon])
+
     def update(self):
+        if self.fused is not None:
+            return self._update_fused()
         b, c = self.buf, self.cfg
         M = c.horizon * b.N * b.A
         obs = b.obs[:c.horizon].reshape(M, b.D)

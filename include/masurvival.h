@@ -161,6 +161,44 @@ int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards
 int mas_sample_actions(int64_t n_rows, const float* logits, int64_t row_stride, uint64_t seed, uint64_t step,
                        int8_t* actions, float* logp, void* stream);
 
+/* Rollout / update side (SURVEY.md 8(a) a24 -- new): the shared-parameter
+ * policy MLP obs_dim -> 256 -> 256 (tanh) -> 16 (the six heads' 15 logits,
+ * then the value) as fused bf16-MFMA kernels with fp32 accumulation.  The
+ * reference has no policy; its demo's act() (demo.py:14-22) is the random
+ * policy this replaces.  All pointers are DEVICE pointers.
+ *
+ * mas_policy_pack fills a packed image of mas_policy_packed_bytes(obs_dim)
+ * bytes from the fp32 parameters W1 [256][obs_dim], b1 [256], W2 [256][256],
+ * b2 [256], W3 [16][256], b3 [16] (row-major, torch nn.Linear layout).
+ *
+ * mas_policy_act: forward of n_rows agent rows of obs [n_rows][obs_dim] fp32
+ * plus Gumbel-max sampling of the six heads with the RNG of
+ * mas_sample_actions; writes actions int8 [n_rows][6], logp and value
+ * [n_rows], and, when x_bf16 != NULL, the bf16 copy of the rows
+ * [n_rows][x_stride] (x_stride a multiple of 8 >= 16*ceil(obs_dim/16), zero
+ * padded) that mas_policy_train reads.
+ *
+ * mas_policy_train: forward of x_bf16 rows, the per-row gradient of the PPO
+ * loss  mean(-min(r A, clip(r, 1-clip, 1+clip) A)) + vf_coef mean((v-ret)^2)
+ * - ent_coef mean(entropy)  (r = exp(logp(actions) - old_logp); `scale` =
+ * 1/rows of the minibatch), and the backward data path; writes feature-major
+ * bf16 h1, h2, dA1, dA2 [256][n_rows] (dA = gradient at the pre-activation)
+ * and dz [16][n_rows], from which the caller forms the weight gradients
+ * (dW1 = dA1 x, dW2 = dA2 h1^T, dW3 = dz h2^T, db = row sums), and
+ * partials [mas_policy_blocks(n_rows)][4] = per-block sums of the clipped
+ * surrogate loss, (v-ret)^2, entropy and the clipped-row count. */
+int64_t mas_policy_packed_bytes(int32_t obs_dim);
+int64_t mas_policy_blocks(int64_t n_rows);
+int mas_policy_pack(int32_t obs_dim, const float* w1, const float* b1, const float* w2, const float* b2,
+                    const float* w3, const float* b3, void* packed, void* stream);
+int mas_policy_act(const void* packed, int32_t obs_dim, int64_t n_rows, const float* obs, void* x_bf16,
+                   int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp, float* value,
+                   void* stream);
+int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
+                     const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
+                     float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
+                     float* partials, void* stream);
+
 /* Diagnostics (synchronises the device): host_out[0] = envs of the last
  * mas_step that left the contact-free physics fast path and ran the general
  * physics kernel (contacts, TOI events, box despawns). */

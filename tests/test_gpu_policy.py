@@ -1,0 +1,148 @@
+"""Fused HIP policy kernels (include/masurvival.h mas_policy_*) against a
+plain torch fp32 restatement of the same MLP and PPO loss.
+
+The kernels compute in bf16 MFMA with fp32 accumulation: the reference uses
+the same bf16-rounded weights and inputs in fp32 arithmetic, so the
+remaining differences are the bf16 rounding of the two hidden activations
+and the accumulation order.  Tolerances (written per assertion below):
+value/log-prob |d| <= 0.03 + 0.03 |ref|; gradients: cosine >= 0.999 and
+relative norm error <= 3 % per parameter tensor; the bf16 input copy is
+exact."""
+import copy
+
+import pytest
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+from masurvival.ppo import (FusedPolicy, PolicyMLP, PPOConfig, evaluate_actions,  # noqa: E402
+                            policy_loss_reference, sample_actions_hip)
+
+
+def _policy(D, seed=0, scale=1.0):
+    torch.manual_seed(seed)
+    p = PolicyMLP(D, 256).cuda()
+    with torch.no_grad():
+        for prm in p.parameters():
+            prm.mul_(scale)
+    return p
+
+
+def _bf16_ref(p):
+    r = copy.deepcopy(p)
+    with torch.no_grad():
+        for prm in r.parameters():
+            prm.copy_(prm.bfloat16().float())
+    return r
+
+
+@pytest.mark.parametrize('D,M', [(160, 4096), (138, 1000 + 13), (468, 777), (160, 32)])
+def test_policy_act_matches_reference(D, M):
+    p = _policy(D, seed=D)
+    fp = FusedPolicy(p, D, torch.device('cuda'))
+    fp.pack()
+    g = torch.Generator(device='cuda').manual_seed(M)
+    obs = torch.randn((M, D), device='cuda', generator=g) * 3.0
+    acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
+    lp = torch.empty((M,), device='cuda')
+    v = torch.empty((M,), device='cuda')
+    xb = torch.full((M, fp.Dp), 7.0, dtype=torch.bfloat16, device='cuda')
+    fp.act(obs, 11, 5, acts, lp, v, xb=xb)
+    # the bf16 copy of the rows is exact, zero padded
+    assert torch.equal(xb[:, :D], obs.bfloat16())
+    assert bool((xb[:, D:] == 0).all())
+    ref = _bf16_ref(p)
+    with torch.no_grad():
+        raw = ref.forward_raw(xb[:, :D].float())
+    # value and log-prob of the drawn actions: |d| <= 0.03 + 0.03 |ref|
+    torch.testing.assert_close(v, raw[:, 15], atol=0.03, rtol=0.03)
+    ref_lp, _ = evaluate_actions(raw[:, :15], acts)
+    torch.testing.assert_close(lp, ref_lp, atol=0.03, rtol=0.03)
+    # the same RNG stream as mas_sample_actions: on the reference logits the
+    # draws agree except where two Gumbel scores are within the logit error
+    a2 = torch.empty_like(acts)
+    lp2 = torch.empty_like(lp)
+    sample_actions_hip(raw.contiguous(), 11, 5, a2, lp2)
+    agree = (a2 == acts).all(1).float().mean().item()
+    assert agree > 0.97, agree
+
+
+def test_policy_act_action_distribution():
+    D, M = 160, 100000
+    p = _policy(D, seed=1, scale=0.0)  # zero weights: the heads' logits are the biases
+    with torch.no_grad():
+        p.head.bias.copy_(torch.linspace(-1.0, 1.0, 16))
+    fp = FusedPolicy(p, D, torch.device('cuda'))
+    fp.pack()
+    obs = torch.randn((M, D), device='cuda')
+    acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
+    lp = torch.empty((M,), device='cuda')
+    v = torch.empty((M,), device='cuda')
+    fp.act(obs, 3, 9, acts, lp, v)
+    b = p.head.bias.detach().bfloat16().float()
+    torch.testing.assert_close(v, b[15].expand(M), atol=0, rtol=0)
+    off = 0
+    for h, n in enumerate((3, 3, 3, 2, 2, 2)):
+        pr = torch.softmax(b[off:off + n], dim=0)
+        freq = torch.bincount(acts[:, h].long(), minlength=n).float() / M
+        assert int(acts[:, h].min()) >= 0 and int(acts[:, h].max()) < n
+        assert torch.allclose(freq, pr, atol=0.01), (h, freq, pr)
+        off += n
+
+
+def _cos(a, b):
+    return float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
+
+
+@pytest.mark.parametrize('D,M', [(160, 8192), (138, 2000 + 7)])
+def test_policy_train_gradients_match_reference(D, M):
+    p = _policy(D, seed=D + 1)
+    cfg = PPOConfig()
+    fp = FusedPolicy(p, D, torch.device('cuda'))
+    fp.pack()
+    g = torch.Generator(device='cuda').manual_seed(7)
+    obs = torch.randn((M, D), device='cuda', generator=g) * 2.0
+    xb = torch.zeros((M, fp.Dp), dtype=torch.bfloat16, device='cuda')
+    acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
+    lp = torch.empty((M,), device='cuda')
+    v = torch.empty((M,), device='cuda')
+    fp.act(obs, 1, 2, acts, lp, v, xb=xb)
+    # a policy that has moved since the rollout: some ratios leave the clip range
+    old_lp = lp + 0.3 * torch.randn((M,), device='cuda', generator=g)
+    adv = torch.randn((M,), device='cuda', generator=g)
+    ret = v + torch.randn((M,), device='cuda', generator=g)
+    loss, pg, vl, ent, cf = fp.grads(xb, acts, old_lp, adv, ret, cfg)
+    ref = _bf16_ref(p)
+    rl, rpg, rvl, rent = policy_loss_reference(ref, xb[:, :D].float(), acts, old_lp, adv, ret, cfg)
+    ref.zero_grad()
+    rl.backward()
+    # loss terms: |d| <= 0.02 + 0.02 |ref|
+    for a, b in ((loss, rl), (pg, rpg), (vl, rvl), (ent, rent)):
+        assert abs(float(a) - float(b)) <= 0.02 + 0.02 * abs(float(b)), (float(a), float(b))
+    assert 0.0 < float(cf) < 1.0
+    for (name, a), b in zip(p.named_parameters(), ref.parameters()):
+        ga, gb = a.grad.float(), b.grad
+        assert _cos(ga, gb) >= 0.999, (name, _cos(ga, gb))
+        assert float((ga.norm() - gb.norm()).abs() / gb.norm()) <= 0.03, name
+
+
+def test_fused_trainer_iteration_on_env():
+    from masurvival.config import C3_CONFIG
+    from masurvival.ppo import PPOTrainer
+    from masurvival.vec_env import VecMaSurvival
+    env = VecMaSurvival(C3_CONFIG, n_envs=1024, auto_reset=True)
+    tr = PPOTrainer(env, PPOConfig(horizon=16), seed=0)
+    assert tr.fused is not None
+    before = [q.detach().clone() for q in tr.policy.parameters()]
+    for _ in range(2):
+        tr.iteration()
+    for k in ('loss', 'pg', 'v', 'entropy', 'clipfrac'):
+        assert torch.isfinite(tr.last_stats[k]), k
+    assert all(not torch.equal(a, b) for a, b in zip(before, tr.policy.parameters()))
+    b = tr.buf
+    assert bool(torch.isfinite(b.adv).all()) and bool(torch.isfinite(b.values).all())
+    hi = torch.tensor([3, 3, 3, 2, 2, 2], device='cuda', dtype=torch.int8)
+    assert bool(((b.actions >= 0) & (b.actions < hi)).all())
+    # the stored update input is the bf16 image of the observations the policy saw
+    assert torch.equal(b.xb[3].view(b.N, b.A, -1)[..., :b.D], b.obs[3].bfloat16())
+    env.close()
