@@ -40,17 +40,25 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 constexpr int kH = 256;   // hidden width
 constexpr int kMT = 8;    // 32-row M-tiles of a hidden layer
 constexpr int kO = 16;    // real outputs of layer 3 (15 logits + value)
-constexpr int kWaves = 4; // waves per workgroup (one per SIMD)
+constexpr int kWaves = 4; // waves per workgroup (one per SIMD; two workgroups per CU)
+constexpr int kLdsFrag = 4608;  // 72 KiB LDS weight stage (16-B fragments): two workgroups per CU
+constexpr int kKc = kLdsFrag / (kMT * 64);  // layer-1 k-steps per stage (9)
+constexpr int kHalf = kMT / 2 * 16 + 8;     // fragment slots of one forward half stage: W2 4 M-tiles + W3 8 k-steps
+static_assert(kHalf * 64 == kLdsFrag, "a forward half stage fills the LDS stage");
+constexpr int kBk0 = 16;                    // backward stage 0: W3^T (8 M-tiles x 2 k-steps)
+constexpr int kBk1 = kMT / 2 * 16;          // backward stages 1, 2: W2^T M-tiles 0..3, 4..7
 
-// packed image, in 16-B fragments (bf8), then f32 biases
+// packed image, in fragment slots of 64 x 16 B (one per lane), then f32
+// biases; every LDS stage is one contiguous range:
+//   w1   [ks1][8]                      layer-1, k-step major
+//   w23  [2][kHalf]                    half q: W2 M-tiles 4q..4q+3 (x16 k-steps), then W3 k-steps 8q..8q+7
+//   wbk  [kBk0 + 2 kBk1]               W3^T (M-tile x 2 k-steps), then W2^T (M-tile x 16 k-steps)
 struct Layout {
     int ks1;  // 16-deep k-steps of layer 1 (ceil(D / 16))
-    __host__ __device__ int64_t w1() const { return 0; }                                  // [ks1][8][64]
-    __host__ __device__ int64_t w2() const { return w1() + (int64_t)ks1 * kMT * 64; }     // [8][16][64]
-    __host__ __device__ int64_t w3() const { return w2() + (int64_t)kMT * 16 * 64; }      // [16][64]
-    __host__ __device__ int64_t w3t() const { return w3() + 16 * 64; }                    // [8][2][64]
-    __host__ __device__ int64_t w2t() const { return w3t() + (int64_t)kMT * 2 * 64; }     // [8][16][64]
-    __host__ __device__ int64_t nfrag() const { return w2t() + (int64_t)kMT * 16 * 64; }
+    __host__ __device__ int64_t w1() const { return 0; }
+    __host__ __device__ int64_t w23() const { return w1() + (int64_t)ks1 * kMT * 64; }
+    __host__ __device__ int64_t wbk() const { return w23() + 2 * kHalf * 64; }
+    __host__ __device__ int64_t nfrag() const { return wbk() + (kBk0 + 2 * kBk1) * 64; }
     // biases (floats) after the fragments: b1p [8][2][16], b2p [8][2][16], b3 [16]
     __host__ __device__ int64_t b1() const { return nfrag() * 4; }
     __host__ __device__ int64_t b2() const { return b1() + kMT * 2 * 16; }
@@ -83,32 +91,36 @@ __global__ void k_pack(int D, int ks1, const float* __restrict__ W1, const float
         const int l = (int)(f & 63), r = l & 31, h = l >> 5;
         const int64_t g = f >> 6;  // fragment index
         float v = 0.0f;
-        if (f < L.w2()) {  // W1: g = ks * 8 + mt, natural k order
+        if (f < L.w23()) {  // W1: g = ks * 8 + mt, natural k order
             const int ks = (int)(g / kMT), mt = (int)(g % kMT);
             const int k = 16 * ks + 8 * h + j;
             v = k < D ? W1[(int64_t)(32 * mt + r) * D + k] : 0.0f;
-        } else if (f < L.w3()) {  // W2: g = mo * 16 + kk (kk = 2 mt + s)
-            const int64_t q = g - L.w2() / 64;
-            const int mo = (int)(q / 16), kk = (int)(q % 16);
-            v = W2[(32 * mo + r) * kH + 32 * (kk >> 1) + prow(kk & 1, h, j)];
-        } else if (f < L.w3t()) {  // W3 (padded to 32 rows): g = kk
-            const int kk = (int)(g - L.w3() / 64);
-            int o = -1;
-            for (int q = 0; q < kO; ++q)
-                if (orow(q) == r) o = q;
-            v = o >= 0 ? W3[o * kH + 32 * (kk >> 1) + prow(kk & 1, h, j)] : 0.0f;
-        } else if (f < L.w2t()) {  // W3pad^T: g = mo * 2 + s
-            const int64_t q = g - L.w3t() / 64;
-            const int mo = (int)(q / 2), s = (int)(q % 2);
-            const int pr = prow(s, h, j);  // padded output row
-            int o = -1;
-            for (int q2 = 0; q2 < kO; ++q2)
-                if (orow(q2) == pr) o = q2;
-            v = o >= 0 ? W3[o * kH + 32 * mo + r] : 0.0f;
-        } else {  // W2^T: g = mt * 16 + kk (kk = 2 mo + s)
-            const int64_t q = g - L.w2t() / 64;
-            const int mt = (int)(q / 16), kk = (int)(q % 16);
-            v = W2[(32 * (kk >> 1) + prow(kk & 1, h, j)) * kH + 32 * mt + r];
+        } else if (f < L.wbk()) {
+            const int q = (int)(g - L.w23() / 64);
+            const int hf = q / kHalf, u = q % kHalf;
+            if (u < kMT / 2 * 16) {  // W2 (mo, kk = 2 mt + s), k permuted
+                const int mo = kMT / 2 * hf + u / 16, kk = u % 16;
+                v = W2[(32 * mo + r) * kH + 32 * (kk >> 1) + prow(kk & 1, h, j)];
+            } else {  // W3 padded to 32 rows, k-step kk
+                const int kk = 8 * hf + (u - kMT / 2 * 16);
+                int o = -1;
+                for (int q2 = 0; q2 < kO; ++q2)
+                    if (orow(q2) == r) o = q2;
+                v = o >= 0 ? W3[o * kH + 32 * (kk >> 1) + prow(kk & 1, h, j)] : 0.0f;
+            }
+        } else {
+            const int q = (int)(g - L.wbk() / 64);
+            if (q < 16) {  // W3pad^T: (mo, s)
+                const int mo = q / 2, sk = q % 2;
+                const int pr = prow(sk, h, j);  // padded output row
+                int o = -1;
+                for (int q2 = 0; q2 < kO; ++q2)
+                    if (orow(q2) == pr) o = q2;
+                v = o >= 0 ? W3[o * kH + 32 * mo + r] : 0.0f;
+            } else {  // W2^T: (mt, kk = 2 mo + s)
+                const int mt = (q - 16) / 16, kk = (q - 16) % 16;
+                v = W2[(32 * (kk >> 1) + prow(kk & 1, h, j)) * kH + 32 * mt + r];
+            }
         }
         frag[t] = (__bf16)v;
         return;
@@ -126,17 +138,28 @@ __global__ void k_pack(int D, int ks1, const float* __restrict__ W1, const float
     }
 }
 
+// timing experiments only (results garbage): 1 no tanh, 2 no sampling, 4 no MFMA, 8 no x loads
+#ifndef MAS_POL_EXP
+#define MAS_POL_EXP 0
+#endif
 __device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c)
 {
+    if (MAS_POL_EXP & 4) return c + (float)a[0];
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// tanh(x) = (e - 1) / (e + 1), e = 2^(2 x log2(e)): one v_exp_f32 and one
+// v_rcp_f32 (~1 ulp each; the result is rounded to bf16 anyway)
 __device__ __forceinline__ float tanh_fast(float x)
 {
+    if (MAS_POL_EXP & 1) return x;
     x = fminf(fmaxf(x, -15.0f), 15.0f);
-    const float e = __expf(2.0f * x);
-    return __fdividef(e - 1.0f, e + 1.0f);
+    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+    return (e - 1.0f) * __builtin_amdgcn_rcpf(e + 1.0f);
 }
+
+__device__ __forceinline__ float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float log_fast(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
 
 __device__ __forceinline__ void load16(const float* __restrict__ p, float* v)
 {
@@ -155,6 +178,10 @@ __device__ __forceinline__ void load16(const float* __restrict__ p, float* v)
 __device__ __forceinline__ bf8 x_frag_f32(const float* __restrict__ obs, int64_t row, bool ok, int D, int k0)
 {
     bf8 f;
+    if (MAS_POL_EXP & 8) {
+        for (int j = 0; j < 8; ++j) f[j] = (__bf16)(float)(row + k0 + j);
+        return f;
+    }
     const float* p = obs + row * D + k0;
     if (ok && (D & 3) == 0 && k0 + 8 <= D) {
         const float4 a = *reinterpret_cast<const float4*>(p);
@@ -163,28 +190,55 @@ __device__ __forceinline__ bf8 x_frag_f32(const float* __restrict__ obs, int64_t
         f[4] = (__bf16)b.x; f[5] = (__bf16)b.y; f[6] = (__bf16)b.z; f[7] = (__bf16)b.w;
     } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = (__bf16)((ok && k0 + j < D) ? p[j] : 0.0f);
+        for (int j = 0; j < 8; ++j)  // column D = 1: the bias column of the update's dW1 GEMM (W1 is 0 there)
+            f[j] = (__bf16)((ok && k0 + j < D) ? p[j] : (ok && k0 + j == D ? 1.0f : 0.0f));
     }
     return f;
 }
 
-// layer 1 over all k-steps into 8 M-tile accumulators, then bias + tanh into
-// the bf16 operand fragments h1[mt][s]
-template <class XF>
-__device__ __forceinline__ void layer1(const bf8* __restrict__ W, const float* __restrict__ b1p, int ks1, int l, XF xf,
-                                       bf8 (&h1)[kMT][2])
+// cooperative copy of n <= kLdsFrag fragments into the LDS stage (all
+// threads of the block): every thread issues all of its loads before the
+// first barrier, so the copy overlaps the slowest wave's previous work and is
+// bandwidth- rather than latency-bound
+constexpr int kStagePer = kLdsFrag / (64 * kWaves);  // fragments per thread (18)
+#ifndef MAS_POL_G
+#define MAS_POL_G 3
+#endif
+#ifndef MAS_POL_KS
+#define MAS_POL_KS 1
+#endif
+template <int G = MAS_POL_G>  // loads in flight per thread (register budget)
+__device__ __forceinline__ void stage(bf8* __restrict__ wl, const bf8* __restrict__ src, int n)
 {
-    const int h = l >> 5;
-    f16v acc[kMT];
+    static_assert(kStagePer % G == 0, "");
+    bf8 t[G];
 #pragma unroll
-    for (int mt = 0; mt < kMT; ++mt) acc[mt] = f16v{};
-#pragma unroll 2
-    for (int ks = 0; ks < ks1; ++ks) {
-        const bf8 x = xf(ks);
-        const bf8* w = W + (int64_t)ks * kMT * 64 + l;
-#pragma unroll
-        for (int mt = 0; mt < kMT; ++mt) acc[mt] = mfma(w[mt * 64], x, acc[mt]);
+    for (int k = 0; k < G; ++k) {
+        const int i = threadIdx.x + k * 64 * kWaves;
+        if (i < n) t[k] = src[i];
     }
+    __syncthreads();  // every wave is done with the previous stage
+#pragma unroll 1
+    for (int g = 0; g < kStagePer; g += G) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int i = threadIdx.x + (g + k) * 64 * kWaves;
+            if (i < n) wl[i] = t[k];
+        }
+        if (g + G < kStagePer) {
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const int i = threadIdx.x + (g + G + k) * 64 * kWaves;
+                if (i < n) t[k] = src[i];
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void tanh_h1(const f16v (&acc)[kMT], const float* __restrict__ b1p, int h,
+                                        bf8 (&h1)[kMT][2])
+{
 #pragma unroll
     for (int mt = 0; mt < kMT; ++mt) {
         float b[16];
@@ -194,30 +248,92 @@ __device__ __forceinline__ void layer1(const bf8* __restrict__ W, const float* _
     }
 }
 
-// layer 2 (by output M-tile) fused with layer 3; h2 kept when KEEP
+// layer 1, x fragments already in registers (KS k-steps, KS <= kKc): one W1
+// stage, 8 M-tile accumulators, then bias + tanh into the bf16 operand
+// fragments h1[mt][s].  Every wave of the block calls it (barriers); `on` =
+// the wave has rows.
+template <int KS>
+__device__ __forceinline__ void layer1_reg(bf8* __restrict__ wl, const bf8* __restrict__ W,
+                                           const float* __restrict__ b1p, int l, bool on, const bf8 (&x)[KS],
+                                           bf8 (&h1)[kMT][2])
+{
+    const int h = l >> 5;
+    f16v acc[kMT];
+#pragma unroll
+    for (int mt = 0; mt < kMT; ++mt) acc[mt] = f16v{};
+#pragma unroll
+    for (int k0 = 0; k0 < KS; k0 += kKc) {
+        const int kn = KS - k0 < kKc ? KS - k0 : kKc;
+        stage(wl, W + k0 * kMT * 64, kn * kMT * 64);
+        if (on) {
+#pragma unroll
+            for (int ks = k0; ks < k0 + kn; ++ks) {
+                const bf8* w = wl + (ks - k0) * kMT * 64 + l;
+#pragma unroll
+                for (int mt = 0; mt < kMT; ++mt) acc[mt] = mfma(w[mt * 64], x[ks], acc[mt]);
+            }
+        }
+    }
+    tanh_h1(acc, b1p, h, h1);
+}
+
+// layer 1 for any obs_dim: W1 staged through LDS in chunks of kKc k-steps, x
+// fragments loaded per k-step by xf(ks)
+template <class XF>
+__device__ __forceinline__ void layer1(bf8* __restrict__ wl, const bf8* __restrict__ W, const float* __restrict__ b1p,
+                                       int ks1, int l, bool on, XF xf, bf8 (&h1)[kMT][2])
+{
+    f16v acc[kMT];
+#pragma unroll
+    for (int mt = 0; mt < kMT; ++mt) acc[mt] = f16v{};
+    for (int k0 = 0; k0 < ks1; k0 += kKc) {
+        const int kn = ks1 - k0 < kKc ? ks1 - k0 : kKc;
+        stage(wl, W + (int64_t)k0 * kMT * 64, kn * kMT * 64);
+        if (on) {
+#pragma unroll 2
+            for (int ks = 0; ks < kn; ++ks) {
+                const bf8 x = xf(k0 + ks);
+                const bf8* w = wl + ks * kMT * 64 + l;
+#pragma unroll
+                for (int mt = 0; mt < kMT; ++mt) acc[mt] = mfma(w[mt * 64], x, acc[mt]);
+            }
+        }
+    }
+    tanh_h1(acc, b1p, l >> 5, h1);
+}
+
+// layer 2 (by output M-tile) fused with layer 3, in two LDS half stages;
+// h2 kept when KEEP.  Every wave of the block calls it (barriers).
 template <bool KEEP>
-__device__ __forceinline__ f16v layers23(const bf8* __restrict__ W2, const bf8* __restrict__ W3,
-                                         const float* __restrict__ b2p, int l, const bf8 (&h1)[kMT][2],
+__device__ __forceinline__ f16v layers23(bf8* __restrict__ wl, const bf8* __restrict__ W23,
+                                         const float* __restrict__ b2p, int l, bool on, const bf8 (&h1)[kMT][2],
                                          bf8 (&h2)[kMT][2])
 {
     const int h = l >> 5;
     f16v z3 = f16v{};
 #pragma unroll
-    for (int mo = 0; mo < kMT; ++mo) {
-        f16v a = f16v{};
-        const bf8* w = W2 + (int64_t)mo * 16 * 64 + l;
+    for (int hf = 0; hf < 2; ++hf) {
+        stage(wl, W23 + hf * kHalf * 64, kHalf * 64);
+        if (!on) continue;
 #pragma unroll
-        for (int kk = 0; kk < 16; ++kk) a = mfma(w[kk * 64], h1[kk >> 1][kk & 1], a);
-        float b[16];
-        load16(b2p + (mo * 2 + h) * 16, b);
-        bf8 f[2];
+        for (int q = 0; q < kMT / 2; ++q) {
+            const int mo = kMT / 2 * hf + q;
+            f16v a = f16v{};
+            const bf8* w = wl + q * 16 * 64 + l;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) f[i >> 3][i & 7] = (__bf16)tanh_fast(a[i] + b[i]);
-        z3 = mfma(W3[(2 * mo) * 64 + l], f[0], z3);
-        z3 = mfma(W3[(2 * mo + 1) * 64 + l], f[1], z3);
-        if (KEEP) {
-            h2[mo][0] = f[0];
-            h2[mo][1] = f[1];
+            for (int kk = 0; kk < 16; ++kk) a = mfma(w[kk * 64], h1[kk >> 1][kk & 1], a);
+            float b[16];
+            load16(b2p + (mo * 2 + h) * 16, b);
+            bf8 f[2];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) f[i >> 3][i & 7] = (__bf16)tanh_fast(a[i] + b[i]);
+            const bf8* w3 = wl + (kMT / 2 * 16 + 2 * q) * 64 + l;
+            z3 = mfma(w3[0], f[0], z3);
+            z3 = mfma(w3[64], f[1], z3);
+            if (KEEP) {
+                h2[mo][0] = f[0];
+                h2[mo][1] = f[1];
+            }
         }
     }
     return z3;
@@ -234,35 +350,56 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
 constexpr int kHeadN[6] = {3, 3, 3, 2, 2, 2};
 constexpr int kHeadOff[6] = {0, 3, 6, 9, 11, 13};
 
-__global__ __launch_bounds__(64 * kWaves) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
+// KS > 0: compile-time k-step count (obs_dim in (16 (KS-1), 16 KS]) with every
+// x fragment loaded up front; KS == 0: any obs_dim, chunked layer 1
+template <int KS>
+__global__ __launch_bounds__(64 * kWaves, 2) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
                                                              int64_t M, const float* __restrict__ obs,
                                                              __bf16* __restrict__ xb, int64_t xb_stride,
                                                              uint64_t seed, uint64_t step, int8_t* __restrict__ act,
                                                              float* __restrict__ logp, float* __restrict__ value)
 {
+    __shared__ bf8 wl[kLdsFrag];
     const Layout Lo{ks1};
     const bf8* F = reinterpret_cast<const bf8*>(packed);
     const float* FB = reinterpret_cast<const float*>(packed);
     const int l = threadIdx.x & 63, h = l >> 5;
     const int64_t row0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32;
-    if (row0 >= M) return;  // wave-uniform
+    const bool on = row0 < M;  // wave-uniform
     const int64_t row = row0 + (l & 31);
     const bool ok = row < M;
     bf8 h1[kMT][2], h2[kMT][2];
-    layer1(F + Lo.w1(), FB + Lo.b1(), ks1, l,
-           [&](int ks) {
-               const bf8 x = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
-               if (xb != nullptr && ok) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x;
-               return x;
-           },
-           h1);
-    const f16v z3 = layers23<false>(F + Lo.w2(), F + Lo.w3(), FB + Lo.b2(), l, h1, h2);
+    if constexpr (KS > 0) {
+        bf8 x[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) x[ks] = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
+        if (xb != nullptr && ok) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x[ks];
+        }
+        layer1_reg<KS>(wl, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
+    } else {
+        layer1(wl, F + Lo.w1(), FB + Lo.b1(), ks1, l, on,
+               [&](int ks) {
+                   const bf8 x = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
+                   if (xb != nullptr && ok) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x;
+                   return x;
+               },
+               h1);
+    }
+    const f16v z3 = layers23<false>(wl, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);  // last barrier
+    if (!on) return;
     if (h != 0 || !ok) return;
+    if (MAS_POL_EXP & 2) {
+        value[row] = z3[0] + z3[15];
+        return;
+    }
     float z[kO];
     const float* b3 = FB + Lo.b3();
 #pragma unroll
     for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
-    // Gumbel-max over each head; the RNG stream of k_sample (mas_capi.hip)
+    // Gumbel-max over each head; the RNG stream of k_sample (mas_capi.hip),
+    // hardware exp2/log2 (the draws agree with k_sample up to ~1 ulp ties)
     const uint64_t base = mix64(seed ^ mix64(step * 0x100000001B3ULL + (uint64_t)row));
     float lp = 0.0f;
     uint32_t packed_a[2] = {0u, 0u};
@@ -274,15 +411,15 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_act(const uint8_t* __res
         for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
         float se = 0.0f;
 #pragma unroll
-        for (int k = 0; k < n; ++k) se += expf(z[off + k] - mx);
-        const float lse = mx + logf(se);
+        for (int k = 0; k < n; ++k) se += exp_fast(z[off + k] - mx);
+        const float lse = mx + log_fast(se);
         int best = 0;
         float bv = -INFINITY, lb = z[off];
 #pragma unroll
         for (int k = 0; k < n; ++k) {
             const uint64_t r = mix64(base + (uint64_t)(hd * 4 + k));
             const float u = ((float)(r >> 40) + 0.5f) * (1.0f / 16777216.0f);
-            const float g = z[off + k] - logf(-logf(u));
+            const float g = z[off + k] - log_fast(-log_fast(u));
             if (g > bv) {
                 bv = g;
                 best = k;
@@ -316,9 +453,10 @@ struct TrainArgs {
     float* partials;        // [gridDim.x][4]: sum pg, sum (v-ret)^2, sum entropy, clipped count
 };
 
-__global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
+template <int KS>
+__global__ __launch_bounds__(64 * kWaves, 2) void k_policy_train(TrainArgs A)
 {
-    __shared__ float red[kWaves][4];
+    __shared__ bf8 wl[kLdsFrag];
     const Layout Lo{A.ks1};
     const bf8* F = reinterpret_cast<const bf8*>(A.packed);
     const float* FB = reinterpret_cast<const float*>(A.packed);
@@ -328,23 +466,31 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
     const int64_t row = row0 + (l & 31);
     const bool ok = row < M;
     float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (row0 < M) {  // wave-uniform
+    const bool on = row0 < M;  // wave-uniform
+    {
         bf8 h1[kMT][2], h2[kMT][2];
-        layer1(F + Lo.w1(), FB + Lo.b1(), A.ks1, l,
-               [&](int ks) {
-                   bf8 x;
-                   if (ok) {
-                       x = *reinterpret_cast<const bf8*>(A.xb + row * A.xb_stride + 16 * ks + 8 * h);
-                   } else {
+        auto xf = [&](int ks) {
+            bf8 x;
+            if (ok) {
+                x = *reinterpret_cast<const bf8*>(A.xb + row * A.xb_stride + 16 * ks + 8 * h);
+            } else {
 #pragma unroll
-                       for (int j = 0; j < 8; ++j) x[j] = (__bf16)0.0f;
-                   }
-                   return x;
-               },
-               h1);
-        const f16v z3 = layers23<true>(F + Lo.w2(), F + Lo.w3(), FB + Lo.b2(), l, h1, h2);
+                for (int j = 0; j < 8; ++j) x[j] = (__bf16)0.0f;
+            }
+            return x;
+        };
+        if constexpr (KS > 0) {
+            bf8 x[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) x[ks] = xf(ks);
+            layer1_reg<KS>(wl, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
+        } else {
+            layer1(wl, F + Lo.w1(), FB + Lo.b1(), A.ks1, l, on, xf, h1);
+        }
+        const f16v z3 = layers23<true>(wl, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);
+        stage(wl, F + Lo.wbk(), kBk0 * 64);  // W3^T
         // feature-major activations for the weight gradients
-        if (ok) {
+        if (on && ok) {
 #pragma unroll
             for (int mt = 0; mt < kMT; ++mt)
 #pragma unroll
@@ -358,7 +504,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
         float dz[kO];
 #pragma unroll
         for (int o = 0; o < kO; ++o) dz[o] = 0.0f;
-        if (h == 0 && ok) {
+        if (on && h == 0 && ok) {
             float z[kO];
             const float* b3 = FB + Lo.b3();
 #pragma unroll
@@ -374,14 +520,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
                 for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
                 float se = 0.0f;
 #pragma unroll
-                for (int k = 0; k < n; ++k) se += expf(z[off + k] - mx);
-                const float lse = mx + logf(se);
+                for (int k = 0; k < n; ++k) se += exp_fast(z[off + k] - mx);
+                const float lse = mx + log_fast(se);
                 float e = 0.0f;
                 const int ak = a[hd];
 #pragma unroll
                 for (int k = 0; k < n; ++k) {
                     lsm[off + k] = z[off + k] - lse;
-                    p[off + k] = expf(lsm[off + k]);
+                    p[off + k] = exp_fast(lsm[off + k]);
                     e -= p[off + k] * lsm[off + k];
                     if (k == ak) lp += lsm[off + k];
                 }
@@ -389,7 +535,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
                 ent += e;
             }
             const float adv = A.adv[row];
-            const float ratio = expf(lp - A.old_logp[row]);
+            const float ratio = exp_fast(lp - A.old_logp[row]);
             const float s1 = ratio * adv;
             const float rc = fminf(fmaxf(ratio, 1.0f - A.clip), 1.0f + A.clip);
             const float s2 = rc * adv;
@@ -422,7 +568,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
         for (int i = 0; i < 16; ++i) dzf[i >> 3][i & 7] = (__bf16)dz[i];
         // dA2 = (W3^T dz) * (1 - h2^2), by M-tile of layer 2
         bf8 da2[kMT][2];
-        const bf8* W3T = F + Lo.w3t() + l;
+        const bf8* W3T = wl + l;
 #pragma unroll
         for (int mo = 0; mo < kMT; ++mo) {
             f16v g = f16v{};
@@ -439,12 +585,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
             }
         }
         // dA1 = (W2^T dA2) * (1 - h1^2), by M-tile of layer 1
-        const bf8* W2T = F + Lo.w2t() + l;
+        const bf8* W2T = wl + l;
 #pragma unroll
         for (int mt = 0; mt < kMT; ++mt) {
+            if (mt % (kMT / 2) == 0)  // W2^T M-tiles 0..3, then 4..7
+                stage(wl, F + Lo.wbk() + (kBk0 + (mt / (kMT / 2)) * kBk1) * 64, kBk1 * 64);
             f16v g = f16v{};
 #pragma unroll
-            for (int kk = 0; kk < 16; ++kk) g = mfma(W2T[(mt * 16 + kk) * 64], da2[kk >> 1][kk & 1], g);
+            for (int kk = 0; kk < 16; ++kk) g = mfma(W2T[((mt % (kMT / 2)) * 16 + kk) * 64], da2[kk >> 1][kk & 1], g);
             if (ok) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -454,19 +602,21 @@ __global__ __launch_bounds__(64 * kWaves) void k_policy_train(TrainArgs A)
             }
         }
     }
-    // per-block loss partials
+    // per-block loss partials (through the LDS stage, after its last reader)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(wl);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         float v = st[k];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (l == 0) red[wv][k] = v;
+        if (l == 0) red[wv * 4 + k] = v;
     }
     __syncthreads();
     if (threadIdx.x < 4) {
         float v = 0.0f;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) v += red[w][threadIdx.x];
+        for (int w = 0; w < kWaves; ++w) v += red[w * 4 + threadIdx.x];
         A.partials[(int64_t)blockIdx.x * 4 + threadIdx.x] = v;
     }
 }
@@ -493,9 +643,10 @@ int64_t policy_blocks(int64_t M) { return (M + 32 * pol::kWaves - 1) / (32 * pol
 hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, void* xb, int64_t xb_stride,
                       uint64_t seed, uint64_t step, int8_t* act, float* logp, float* value, hipStream_t s)
 {
-    hipLaunchKernelGGL(pol::k_policy_act, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s,
-                       (const uint8_t*)packed, D, (D + 15) / 16, M, obs, (__bf16*)xb, xb_stride, seed, step, act,
-                       logp, value);
+    const int ks1 = (D + 15) / 16;
+    auto k = !MAS_POL_KS ? pol::k_policy_act<0> : ks1 == 10 ? pol::k_policy_act<10> : ks1 == 9 ? pol::k_policy_act<9> : pol::k_policy_act<0>;
+    hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
+                       ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, act, logp, value);
     return hipGetLastError();
 }
 
@@ -524,7 +675,8 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     A.da2 = (__bf16*)da2;
     A.dz = (__bf16*)dz;
     A.partials = partials;
-    hipLaunchKernelGGL(pol::k_policy_train, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, A);
+    auto k = !MAS_POL_KS ? pol::k_policy_train<0> : A.ks1 == 10 ? pol::k_policy_train<10> : A.ks1 == 9 ? pol::k_policy_train<9> : pol::k_policy_train<0>;
+    hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, A);
     return hipGetLastError();
 }
 

@@ -219,7 +219,8 @@ class FusedPolicy:
     def __init__(self, policy: 'PolicyMLP', obs_dim: int, device):
         self.lib = load_library()
         self.policy, self.D, self.device = policy, int(obs_dim), device
-        self.Dp = 16 * ((self.D + 15) // 16)
+        self.Dp = 16 * ((self.D + 15) // 16)      # columns the kernels read / write
+        self.Dx = 16 * ((self.D + 1 + 15) // 16)  # row stride of x: room for the bias column at index D
         w1, w2 = policy.body[0].weight, policy.body[2].weight
         assert w1.shape == (256, self.D) and w2.shape == (256, 256) and policy.head.weight.shape == (16, 256)
         self.packed = torch.empty((int(self.lib.mas_policy_packed_bytes(self.D)),), dtype=torch.uint8, device=device)
@@ -236,16 +237,23 @@ class FusedPolicy:
         check(self.lib.mas_policy_pack(self.D, *[ctypes.c_void_p(t.data_ptr()) for t in ts],
                                        ctypes.c_void_p(self.packed.data_ptr()), self._stream()))
 
+    def x_buffer(self, *shape):
+        """bf16 policy-input rows [*shape, Dx] with the bias column (index D) = 1."""
+        x = torch.zeros((*shape, self.Dx), dtype=torch.bfloat16, device=self.device)
+        x[..., self.D] = 1.0
+        return x
+
     @torch.no_grad()
     def act(self, obs, seed, step, actions, logp, value, xb=None):
         """obs [M, D] fp32 rows -> actions int8 [M, 6], logp, value [M];
-        xb [M, Dp] bf16 (optional) receives the rows as the update reads them."""
+        xb [M, Dx] bf16 (optional, from x_buffer) receives the rows as the
+        update reads them."""
         M = obs.shape[0]
         assert obs.is_contiguous() and obs.dtype == torch.float32 and obs.shape[1] == self.D
         assert actions.is_contiguous() and logp.is_contiguous() and value.is_contiguous()
         xp = ctypes.c_void_p(xb.data_ptr()) if xb is not None else None
         check(self.lib.mas_policy_act(ctypes.c_void_p(self.packed.data_ptr()), self.D, M, ctypes.c_void_p(obs.data_ptr()),
-                                      xp, self.Dp, int(seed), int(step), ctypes.c_void_p(actions.data_ptr()),
+                                      xp, self.Dx, int(seed), int(step), ctypes.c_void_p(actions.data_ptr()),
                                       ctypes.c_void_p(logp.data_ptr()), ctypes.c_void_p(value.data_ptr()),
                                       self._stream()))
 
@@ -253,7 +261,11 @@ class FusedPolicy:
         if self._bufs is None or self._bufs['M'] != M:
             bf = dict(dtype=torch.bfloat16, device=self.device)
             nb = int(self.lib.mas_policy_blocks(M))
-            self._bufs = {'M': M, 'h1': torch.empty((256, M), **bf), 'h2': torch.empty((256, M), **bf),
+            # h1 / h2 carry a row of ones (row 256): dW @ [h; 1]^T yields the bias gradient as its last column
+            h1, h2 = torch.empty((257, M), **bf), torch.empty((257, M), **bf)
+            h1[256] = 1.0
+            h2[256] = 1.0
+            self._bufs = {'M': M, 'h1': h1, 'h2': h2,
                           'da1': torch.empty((256, M), **bf), 'da2': torch.empty((256, M), **bf),
                           'dz': torch.empty((16, M), **bf),
                           'part': torch.empty((nb, 4), dtype=torch.float32, device=self.device)}
@@ -263,22 +275,22 @@ class FusedPolicy:
         """Sets .grad of the policy parameters to the gradient of the PPO loss
         (mean over the M rows) and returns (loss, pg, v, entropy, clipfrac)."""
         M = xb.shape[0]
-        assert xb.dtype == torch.bfloat16 and xb.shape[1] == self.Dp and xb.is_contiguous()
+        assert xb.dtype == torch.bfloat16 and xb.shape[1] == self.Dx and xb.is_contiguous()
         for t in (actions, old_logp, adv, ret):
             assert t.is_contiguous()
         B = self._buffers(M)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        check(self.lib.mas_policy_train(ptr(self.packed), self.D, M, ptr(xb), self.Dp, ptr(actions), ptr(old_logp),
+        check(self.lib.mas_policy_train(ptr(self.packed), self.D, M, ptr(xb), self.Dx, ptr(actions), ptr(old_logp),
                                         ptr(adv), ptr(ret), cfg.clip, cfg.vf_coef, cfg.ent_coef, 1.0 / M, ptr(B['h1']),
                                         ptr(B['h2']), ptr(B['da1']), ptr(B['da2']), ptr(B['dz']), ptr(B['part']),
                                         self._stream()))
         p = self.policy
         l1, l2, l3 = p.body[0], p.body[2], p.head
-        grads = {
-            l3.weight: _splitk_nt(B['dz'], B['h2']), l3.bias: B['dz'].sum(1, dtype=torch.float32),
-            l2.weight: _splitk_nt(B['da2'], B['h1']), l2.bias: B['da2'].sum(1, dtype=torch.float32),
-            l1.weight: _splitk_nn(B['da1'], xb)[:, :self.D], l1.bias: B['da1'].sum(1, dtype=torch.float32),
-        }
+        g3 = _splitk_nt(B['dz'], B['h2'])              # [16, 257]
+        g2 = _splitk_nt(B['da2'], B['h1'])             # [256, 257]
+        g1 = _splitk_nn(B['da1'], xb[:, :self.D + 1])  # [256, D + 1]
+        grads = {l3.weight: g3[:, :256], l3.bias: g3[:, 256], l2.weight: g2[:, :256], l2.bias: g2[:, 256],
+                 l1.weight: g1[:, :self.D], l1.bias: g1[:, self.D]}
         for prm, g in grads.items():
             if prm.grad is None:
                 prm.grad = g.to(prm.dtype).contiguous()
@@ -366,7 +378,7 @@ class PPOTrainer:
         if fused:
             self.fused = FusedPolicy(self.policy, env.obs_dim, self.device)
             b = self.buf
-            self.buf.xb = torch.zeros((b.T, b.N * b.A, self.fused.Dp), dtype=torch.bfloat16, device=self.device)
+            self.buf.xb = self.fused.x_buffer(b.T, b.N * b.A)
             M = b.N * b.A
             self._boot = (torch.empty((M, 6), dtype=torch.int8, device=self.device),
                           torch.empty((M,), dtype=torch.float32, device=self.device))
@@ -439,7 +451,7 @@ class PPOTrainer:
             order = torch.randperm(c.minibatches, generator=torch.Generator().manual_seed(self.steps_taken))
             for k in order.tolist():
                 sl = slice(k * tc, (k + 1) * tc)
-                xb = b.xb[sl].reshape(-1, self.fused.Dp)
+                xb = b.xb[sl].reshape(-1, self.fused.Dx)
                 M = xb.shape[0]
                 loss, pg, vl, ent, cf = self.fused.grads(xb, b.actions[sl].reshape(M, 6), b.logp[sl].reshape(M),
                                                          b.adv[sl].reshape(M), b.ret[sl].reshape(M), c)

@@ -175,8 +175,10 @@ int mas_sample_actions(int64_t n_rows, const float* logits, int64_t row_stride, 
  * plus Gumbel-max sampling of the six heads with the RNG of
  * mas_sample_actions; writes actions int8 [n_rows][6], logp and value
  * [n_rows], and, when x_bf16 != NULL, the bf16 copy of the rows
- * [n_rows][x_stride] (x_stride a multiple of 8 >= 16*ceil(obs_dim/16), zero
- * padded) that mas_policy_train reads.
+ * [n_rows][x_stride] (x_stride a multiple of 8 >= 16*ceil(obs_dim/16)) that
+ * mas_policy_train reads: columns [0, 16*ceil(obs_dim/16)) are written, the
+ * row's obs_dim values, then 1.0 in column obs_dim (a bias column for the
+ * caller's dW1 GEMM) when it falls in that range, then zeros.
  *
  * mas_policy_train: forward of x_bf16 rows, the per-row gradient of the PPO
  * loss  mean(-min(r A, clip(r, 1-clip, 1+clip) A)) + vf_coef mean((v-ret)^2)
@@ -184,7 +186,9 @@ int mas_sample_actions(int64_t n_rows, const float* logits, int64_t row_stride, 
  * 1/rows of the minibatch), and the backward data path; writes feature-major
  * bf16 h1, h2, dA1, dA2 [256][n_rows] (dA = gradient at the pre-activation)
  * and dz [16][n_rows], from which the caller forms the weight gradients
- * (dW1 = dA1 x, dW2 = dA2 h1^T, dW3 = dz h2^T, db = row sums), and
+ * (dW1 = dA1 x, dW2 = dA2 h1^T, dW3 = dz h2^T, db = row sums; a row of ones
+ * appended to h1 / h2 and the bias column of x give the db's from the same
+ * GEMMs), and
  * partials [mas_policy_blocks(n_rows)][4] = per-block sums of the clipped
  * surrogate loss, (v-ret)^2, entropy and the clipped-row count. */
 int64_t mas_policy_packed_bytes(int32_t obs_dim);

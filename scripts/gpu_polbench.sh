@@ -1,0 +1,8 @@
+#!/bin/bash
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/polbench
+mkdir -p $O
+cd $R
+L=gym-ma-survival-2d_amd/masurvival/_lib
+timeout -k 10 300 python scripts/policy_bench.py > $O/polbench.log 2>&1 || exit $?
+echo ok

@@ -46,11 +46,14 @@ def test_policy_act_matches_reference(D, M):
     acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
     lp = torch.empty((M,), device='cuda')
     v = torch.empty((M,), device='cuda')
-    xb = torch.full((M, fp.Dp), 7.0, dtype=torch.bfloat16, device='cuda')
+    xb = torch.full((M, fp.Dx), 7.0, dtype=torch.bfloat16, device='cuda')
     fp.act(obs, 11, 5, acts, lp, v, xb=xb)
-    # the bf16 copy of the rows is exact, zero padded
+    # the bf16 copy of the rows is exact; written columns [0, Dp): the row,
+    # then the bias column (1.0 at index D) when it falls inside, then zeros
     assert torch.equal(xb[:, :D], obs.bfloat16())
-    assert bool((xb[:, D:] == 0).all())
+    if D < fp.Dp:
+        assert bool((xb[:, D] == 1).all()) and bool((xb[:, D + 1:fp.Dp] == 0).all())
+    assert bool((xb[:, fp.Dp:] == 7).all())
     ref = _bf16_ref(p)
     with torch.no_grad():
         raw = ref.forward_raw(xb[:, :D].float())
@@ -102,7 +105,7 @@ def test_policy_train_gradients_match_reference(D, M):
     fp.pack()
     g = torch.Generator(device='cuda').manual_seed(7)
     obs = torch.randn((M, D), device='cuda', generator=g) * 2.0
-    xb = torch.zeros((M, fp.Dp), dtype=torch.bfloat16, device='cuda')
+    xb = fp.x_buffer(M)
     acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
     lp = torch.empty((M,), device='cuda')
     v = torch.empty((M,), device='cuda')
