@@ -269,6 +269,51 @@ __device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, S
     }
 }
 
+// update_seen for the single camera slot `cam` (k_cameras runs one lane per
+// (env, camera) and ORs the lanes' masks): same candidate order and rays as
+// update_seen restricted to camera cam, whose camera-list position is its
+// rank among the alive agents.
+template <class C>
+__device__ __forceinline__ void update_seen_cam(const EnvL<C>& L, const Params& P, Scr<C>& scr, const FixTab<C>& T,
+                                                int cam)
+{
+#pragma unroll
+    for (int k = 0; k < C::NB; ++k) scr.sn(k) = 0u;
+    if (!bit(L.alive_m, cam)) return;
+    const int p = __popc(L.alive_m & ((1u << cam) - 1u));
+    V2 pos = mk(0.0f, 0.0f);
+    float ang = 0.0f;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+        if (i == cam) { pos = opq(L.c[i]); ang = opq(L.a[i]); }
+    const Rot q = rot_of(ang);
+    int np = 0;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b)
+        if (b < L.nbox && poly_test_point(P.cone, pos, q, L.bp[b])) scr.pr(np++) = BIdx<C>::box + b;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b)
+        if (b < L.nbi && poly_test_point(P.cone, pos, q, L.ip[b])) scr.pr(np++) = BIdx<C>::bitem + b;
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h)
+        if (h < L.nheal && poly_test_point(P.cone, pos, q, L.hp[h])) scr.pr(np++) = BIdx<C>::heal + h;
+#pragma unroll
+    for (int w = 0; w < kNumWalls; ++w)
+        if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) scr.pr(np++) = BIdx<C>::wall + w;
+#pragma unroll
+    for (int j = 0; j < C::AM; ++j)
+        if (j != cam && bit(L.alive_m, j) && poly_test_point(P.cone, pos, q, L.c[j]))
+            scr.pr(np++) = BIdx<C>::agent + j;
+    const float eps1 = (float)(1.0 + 1e-6);
+    for (int t = 0; t < np; ++t) {
+        const int body = (int)scr.pr(t);
+        const V2 oc = mk(T.px(body), T.py(body));
+        const V2 d = sub(oc, pos);
+        const V2 end = add(pos, scl(eps1, d));
+        if (ray_cast_tab(L, P, T, pos, end) == body) scr.sn(body) |= 1u << p;
+    }
+}
+
 // Cameras.seen <-> state bytes (kGSeen): byte k = camera-position mask of body k
 template <class C>
 __device__ __forceinline__ void seen_pack(EnvL<C>& L, Scr<C>& scr)
