@@ -304,6 +304,7 @@ __device__ __forceinline__ void update_seen_cam(const EnvL<C>& L, const Params& 
     for (int j = 0; j < C::AM; ++j)
         if (j != cam && bit(L.alive_m, j) && poly_test_point(P.cone, pos, q, L.c[j]))
             scr.pr(np++) = BIdx<C>::agent + j;
+    MAS_PROF(P, 13);
     const float eps1 = (float)(1.0 + 1e-6);
     for (int t = 0; t < np; ++t) {
         const int body = (int)scr.pr(t);
