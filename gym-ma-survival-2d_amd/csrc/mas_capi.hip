@@ -295,6 +295,7 @@ struct mas_handle {
     uint32_t* state;
     uint64_t* seedbuf;
     int* phys;  // [N] env list + [1] count (k_phys_fast -> general path)
+    uint8_t* gen_flag;  // [N] env left the fast path this step
     float* sweep;
     mas_obs_layout layout;
 };
@@ -504,6 +505,10 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->sweep = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * 8 * sizeof(float));
     h->P.sweep = h->sweep;
+    h->gen_flag = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&h->gen_flag, (size_t)n_envs);
+    if (e == hipSuccess) e = hipMemset(h->gen_flag, 0, (size_t)n_envs);
+    h->P.gen_flag = h->gen_flag;
     h->P.phys_list = h->phys;
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
 #ifdef MAS_PROFILE
@@ -512,8 +517,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
 #endif
     if (e != hipSuccess) {
         std::string msg = std::string("mas_create: ") + hipGetErrorString(e);
-        if (h->state) hipFree(h->state);
-        delete h;
+        mas_destroy(h);
         return fail(MAS_ERR_HIP, msg);
     }
     *out = h;
@@ -528,6 +532,7 @@ int mas_destroy(mas_handle* h)
     if (h->P.prof) (void)hipFree(h->P.prof);
     if (h->phys) (void)hipFree(h->phys);
     if (h->sweep) (void)hipFree(h->sweep);
+    if (h->gen_flag) (void)hipFree(h->gen_flag);
     delete h;
     return MAS_OK;
 }

@@ -75,7 +75,8 @@ struct Params {
     int o_agent, o_bi, o_bim, o_bs, o_bsm, o_box, o_boxm, o_hs, o_hsm, o_heal, o_healm, o_oth, o_othm, o_zone;
     int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
     int* phys_count;  // number of them
-    float* sweep;     // [list position][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
+    uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)
+    float* sweep;     // [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
 
@@ -87,7 +88,7 @@ __device__ __forceinline__ void prof_mark(const Params& P, int k)
 {
     __shared__ unsigned long long t_last;
     unsigned long long t = wall_clock64();
-    if (threadIdx.x == 0) {
+    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) {  // first active lane
         if (k >= 0) atomicAdd(&P.prof[k], t - t_last);
         t_last = t;
     }

@@ -223,8 +223,11 @@ MAS_HD float ray_poly(const Poly4& P, V2 xp, Rot xq, V2 p1w, V2 p2w, float maxf)
     float lower = 0.0f, upper = maxf;
     int index = -1;
     bool miss = false;
+    // unrolled (static edge indices keep the polygon in registers); the
+    // iterations after a miss change nothing, as Box2D's early return
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
-        if (miss) break;
+        if (miss) continue;
         float num = dot(P.n[i], sub(P.v[i], p1));
         float den = dot(P.n[i], d);
         if (den == 0.0f) {

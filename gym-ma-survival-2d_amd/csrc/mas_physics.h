@@ -1037,6 +1037,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
                 need |= 1u << s;
             }
         }
+        MAS_PROF(P, 21);
         // (2) full b2TimeOfImpact for the rest (runtime loop: one code copy)
 #pragma unroll 1
         while (need) {
@@ -1054,6 +1055,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
             put(toi, s, alpha);
             valid |= 1u << s;
         }
+        MAS_PROF(P, 22);
         // (3) minimum over the enabled contacts (ties: lowest canonical index)
         float minAlpha = 1.0f;
         int minS = -1;
@@ -1161,6 +1163,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
         sw.c = cB;
         sw.a = aB;
         valid = 0;
+        MAS_PROF(P, 24);
     }
     put(L.c, I, sw.c);
     put(L.a, I, sw.a);

@@ -142,6 +142,17 @@ __global__ void k_pack(int D, int ks1, const float* __restrict__ W1, const float
 #ifndef MAS_POL_EXP
 #define MAS_POL_EXP 0
 #endif
+// scheduling strategy hint for the MFMA + LDS-read loops (A/B builds)
+#ifndef MAS_POL_IGLP
+#define MAS_POL_IGLP -1
+#endif
+__device__ __forceinline__ void iglp()
+{
+#if MAS_POL_IGLP >= 0
+    __builtin_amdgcn_iglp_opt(MAS_POL_IGLP);
+#endif
+}
+
 __device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c)
 {
     if (MAS_POL_EXP & 4) return c + (float)a[0];
@@ -320,6 +331,7 @@ __device__ __forceinline__ f16v layers23(bf8* __restrict__ wl, const bf8* __rest
             const int mo = kMT / 2 * hf + q;
             f16v a = f16v{};
             const bf8* w = wl + q * 16 * 64 + l;
+            iglp();
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk) a = mfma(w[kk * 64], h1[kk >> 1][kk & 1], a);
             float b[16];

@@ -768,11 +768,18 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
     const int A = P.A;
     // queue_actions (masurvival_env.py:741-755): alive agents only
     int ac[C::AM][6];
+    // every byte load unconditional (index clamped into the env's row): the
+    // loads issue together instead of one branch + load + wait each
+    int8_t raw[C::AM][6];
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) raw[i][k] = act[min(i, A - 1) * 6 + k];
 #pragma unroll
     for (int i = 0; i < C::AM; ++i)
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            int x = i < A ? (int)act[i * 6 + k] : 0;
+            int x = i < A ? (int)raw[i][k] : 0;
             int hi = k < 3 ? 2 : 1;
             ac[i][k] = x < 0 ? 0 : (x > hi ? hi : x);
         }
@@ -892,6 +899,40 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
     L.stats[18] += (float)uses_box;
 }
 
+// the agent-static rows of the contact memory (touching words and impulses)
+// in registers, for the box despawn compaction of box_health
+template <class C>
+struct ContRowsReg {
+    uint32_t t[C::AM];
+    float ni[C::AM][C::NS], ti[C::AM][C::NS];
+    template <class KT>
+    __device__ void load(const KT& K)
+    {
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            t[i] = K.ast(i);
+#pragma unroll
+            for (int s = 0; s < C::NS; ++s) {
+                ni[i][s] = K.asni(i, s);
+                ti[i][s] = K.asti(i, s);
+            }
+        }
+    }
+    template <class KT>
+    __device__ void store(const KT& K) const
+    {
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            K.set_ast(i, t[i]);
+#pragma unroll
+            for (int s = 0; s < C::NS; ++s) {
+                K.set_asni(i, s, ni[i][s]);
+                K.set_asti(i, s, ti[i][s]);
+            }
+        }
+    }
+};
+
 // boxes: Health.post_step + Object / OwnedObject despawn (semantics.py:429-435,
 // 858-861, 907-912) -- the first post_step hook (dict order: boxes group
 // before agents), run at the start of k_cameras.  Returns true when the box /
@@ -916,6 +957,11 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
         }
         if (any_dead) {
             changed = true;
+            // the agent-static contact rows, read once into registers (one
+            // round trip instead of a load -> store -> load chain per word),
+            // shifted with the boxes, written back once
+            ContRowsReg<C> R;
+            R.load(K);
             // stable compaction; dead boxes queue (pos, copy_shape(proto), cause)
             int wi = 0;
 #pragma unroll
@@ -939,11 +985,11 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
                         L.bp[k] = p; L.bhx[k] = hx; L.bhy[k] = hy; L.bmeta[k] = meta; L.bhealth[k] = hl;
 #pragma unroll
                         for (int i = 0; i < C::AM; ++i) {
-                            const uint32_t at = K.ast(i);
+                            const uint32_t at = R.t[i];
                             bool tb = bit(at, kNumWalls + b);
-                            K.set_ast(i, tb ? (at | (1u << (kNumWalls + k))) : (at & ~(1u << (kNumWalls + k))));
-                            K.set_asni(i, kNumWalls + k, K.asni(i, kNumWalls + b));
-                            K.set_asti(i, kNumWalls + k, K.asti(i, kNumWalls + b));
+                            R.t[i] = tb ? (at | (1u << (kNumWalls + k))) : (at & ~(1u << (kNumWalls + k)));
+                            R.ni[i][kNumWalls + k] = R.ni[i][kNumWalls + b];
+                            R.ti[i][kNumWalls + k] = R.ti[i][kNumWalls + b];
                         }
                     }
                     ++wi;
@@ -955,11 +1001,12 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
                 if (k < wi) continue;
 #pragma unroll
                 for (int i = 0; i < C::AM; ++i) {
-                    K.set_ast(i, K.ast(i) & ~(1u << (kNumWalls + k)));
-                    K.set_asni(i, kNumWalls + k, 0.0f);
-                    K.set_asti(i, kNumWalls + k, 0.0f);
+                    R.t[i] &= ~(1u << (kNumWalls + k));
+                    R.ni[i][kNumWalls + k] = 0.0f;
+                    R.ti[i][kNumWalls + k] = 0.0f;
                 }
             }
+            R.store(K);
         }
     }
     return changed;
@@ -967,8 +1014,10 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
 
 // agents: Cameras.post_step over the pre-despawn list runs between step_phys
 // and step_post (k_cameras); step_post reads and compacts its bytes.
-template <class C>
-__device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const Cont<C>& K, float* rew)
+// K: the contact memory, touched only on deaths (k_post passes the HBM image
+// directly).  rng_used: the PCG64 stream advanced (DeathDrop draws).
+template <class C, class KT>
+__device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const KT& K, float* rew, bool& rng_used)
 {
     const int A = P.A;
     // agents: Health.post_step -> despawn dead (id order): TrackDeaths, IndexBodies,
@@ -980,6 +1029,7 @@ __device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const Con
         kill_cause[i] = kCauseNone;
         if (bit(L.alive_m, i) && L.health[i] <= 0) died |= 1u << i;
     }
+    rng_used = died != 0;
     if (died) {
         int total = 0;
 #pragma unroll
@@ -1011,6 +1061,7 @@ __device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const Con
             }
             L.inv_n[i] = 0;
         }
+        uint32_t aat = K.aat();  // one load: the agent-agent touching word
 #pragma unroll
         for (int i = 0; i < C::AM; ++i) {
             if (!bit(died, i)) continue;
@@ -1024,11 +1075,12 @@ __device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const Con
             for (int j = 0; j < C::AM; ++j) {
                 if (j == i) continue;
                 int p = j < i ? aa_index<C::AM>(j, i) : aa_index<C::AM>(i, j);
-                K.set_aat(K.aat() & ~(1u << p));
+                aat &= ~(1u << p);
                 K.set_aani(p, 0.0f);
                 K.set_aati(p, 0.0f);
             }
         }
+        K.set_aat(aat);
     }
     // AutoPickup.post_step (semantics.py:278-283): every agent's list first
     {

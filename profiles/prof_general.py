@@ -1,0 +1,58 @@
+"""Per-phase wave time of the general physics path (k_gen_solve, k_gen_toi)
+from the profiling build (libmas_prof.so, `make -C gym-ma-survival-2d_amd/csrc
+prof`).  Marks: mas_kernels.inc / mas_physics.h MAS_PROF; the first active
+lane of each wave adds the 100 MHz constant-clock time since the previous
+mark.  Prints the mean per ACTIVE wave per step (us).
+usage: python profiles/prof_general.py [n_envs] [steps]"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'gym-ma-survival-2d_amd'))
+
+import torch  # noqa: E402
+
+from masurvival import abi  # noqa: E402
+
+SOLVE = {0: 'solve: state + contact load', 1: 'solve: collide', 2: 'solve: island solve', 4: 'solve: store'}
+TOI = {20: 'toi: load + sweep', 21: 'toi: reject pre-tests', 22: 'toi: b2TimeOfImpact', 24: 'toi: TOI events',
+       23: 'toi: min / exit'}
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    lib = abi.load_library(os.path.join(os.path.dirname(abi.LIB_PATH), 'libmas_prof.so'))
+    lib.mas_prof_read.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
+    from masurvival.config import NAMED_CONFIGS
+    from masurvival.vec_env import VecMaSurvival
+    env = VecMaSurvival(NAMED_CONFIGS['2v2'], n_envs=n, auto_reset=True)
+    buf = (ctypes.c_ulonglong * 64)()
+    env.reset()
+    gen = torch.Generator(device=env.device)
+    gen.manual_seed(0)
+    hi = torch.tensor([3, 3, 3, 2, 2, 2], device=env.device)
+    acts = lambda: (torch.rand((n, env.n_agents, 6), generator=gen, device=env.device) * hi).to(torch.int8)  # noqa
+    for _ in range(150):  # let agents reach walls and each other
+        env.step(acts())
+    abi.check(lib.mas_prof_read(env._h, buf))
+    gen_envs = 0
+    for _ in range(steps):
+        env.step(acts())
+        gen_envs += env.debug_counters()['phys_general_envs']
+    abi.check(lib.mas_prof_read(env._h, buf))
+    g = gen_envs / steps
+    ws, wt = 2 * (g + 63) // 64, 2 * (4 * g + 63) // 64  # active waves per step (2 world steps)
+    print(f'# general-path envs per step {g:.0f}; active waves per step: solve {ws:.0f}, toi {wt:.0f}')
+    for tab, w in ((SOLVE, ws), (TOI, wt)):
+        tot = 0.0
+        for k, name in tab.items():
+            t = buf[k] * 0.01 / (w * steps)
+            tot += t
+            print(f'{name:30s} {t:8.2f} us per active wave')
+        print(f'{"total":30s} {tot:8.2f}')
+
+
+if __name__ == '__main__':
+    main()

@@ -3,5 +3,5 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/profcam
 mkdir -p $O
 cd $R
-timeout -k 10 200 python profiles/prof_cameras.py > $O/prof_cameras.log 2>&1 || exit $?
+timeout -k 10 200 python profiles/prof_general.py > $O/prof_general.log 2>&1 || exit $?
 echo ok
