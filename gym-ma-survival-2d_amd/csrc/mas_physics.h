@@ -982,6 +982,10 @@ MAS_HD bool toi_reject(const StaticG& g, V2 p0, V2 p1, float rB)
     }
     ex += R;
     ey += R;
+    // the segment's box against the grown rectangle first: no divisions, and
+    // it settles the far statics (most of them); then the exact slab test
+    if (fminf(l0.x, l1.x) > ex || fmaxf(l0.x, l1.x) < -ex || fminf(l0.y, l1.y) > ey || fmaxf(l0.y, l1.y) < -ey)
+        return true;
     float tmin = 0.0f, tmax = 1.0f;
     V2 d = sub(l1, l0);
     if (fabsf(d.x) < 1e-12f) {

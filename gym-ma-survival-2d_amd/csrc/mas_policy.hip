@@ -185,6 +185,21 @@ __device__ __forceinline__ void load16(const float* __restrict__ p, float* v)
     }
 }
 
+// x fragment of k-step ks for this lane's row from fp32 obs [M][D], for
+// D % 4 == 0 and a complete k-step: unconditional 16-B loads (row clamped
+// into range by the caller), the row of an out-of-range lane zeroed after
+__device__ __forceinline__ bf8 x_frag_f32_full(const float* __restrict__ obs, int64_t row, bool ok, int D, int k0)
+{
+    const float* p = obs + row * D + k0;
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    const float z = ok ? 1.0f : 0.0f;
+    bf8 f;
+    f[0] = (__bf16)(a.x * z); f[1] = (__bf16)(a.y * z); f[2] = (__bf16)(a.z * z); f[3] = (__bf16)(a.w * z);
+    f[4] = (__bf16)(b.x * z); f[5] = (__bf16)(b.y * z); f[6] = (__bf16)(b.z * z); f[7] = (__bf16)(b.w * z);
+    return f;
+}
+
 // x fragment of k-step ks for this lane's row from fp32 obs [M][D]
 __device__ __forceinline__ bf8 x_frag_f32(const float* __restrict__ obs, int64_t row, bool ok, int D, int k0)
 {
@@ -207,43 +222,22 @@ __device__ __forceinline__ bf8 x_frag_f32(const float* __restrict__ obs, int64_t
     return f;
 }
 
-// cooperative copy of n <= kLdsFrag fragments into the LDS stage (all
-// threads of the block): every thread issues all of its loads before the
-// first barrier, so the copy overlaps the slowest wave's previous work and is
-// bandwidth- rather than latency-bound
+// cooperative copy of n <= kLdsFrag fragments (n a multiple of 64) into the
+// LDS stage by LDS-DMA (global_load_lds_dwordx4: no registers, every load of
+// the stage in flight at once, one wait), between two block barriers
 constexpr int kStagePer = kLdsFrag / (64 * kWaves);  // fragments per thread (18)
-#ifndef MAS_POL_G
-#define MAS_POL_G 3
-#endif
-#ifndef MAS_POL_KS
-#define MAS_POL_KS 1
-#endif
-template <int G = MAS_POL_G>  // loads in flight per thread (register budget)
+typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void stage(bf8* __restrict__ wl, const bf8* __restrict__ src, int n)
 {
-    static_assert(kStagePer % G == 0, "");
-    bf8 t[G];
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-        const int i = threadIdx.x + k * 64 * kWaves;
-        if (i < n) t[k] = src[i];
-    }
     __syncthreads();  // every wave is done with the previous stage
-#pragma unroll 1
-    for (int g = 0; g < kStagePer; g += G) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-        for (int k = 0; k < G; ++k) {
-            const int i = threadIdx.x + (g + k) * 64 * kWaves;
-            if (i < n) wl[i] = t[k];
-        }
-        if (g + G < kStagePer) {
-#pragma unroll
-            for (int k = 0; k < G; ++k) {
-                const int i = threadIdx.x + (g + G + k) * 64 * kWaves;
-                if (i < n) t[k] = src[i];
-            }
-        }
+    for (int k = 0; k < kStagePer; ++k) {
+        const int i0 = (int)(threadIdx.x & ~63u) + k * 64 * kWaves;  // the wave's first fragment
+        if (i0 < n)  // wave-uniform
+            __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane), (lds_void*)(wl + i0), 16, 0, 0);
     }
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 }
 
@@ -383,8 +377,14 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_policy_act(const uint8_t* __
     bf8 h1[kMT][2], h2[kMT][2];
     if constexpr (KS > 0) {
         bf8 x[KS];
+        if ((D & 3) == 0 && D == 16 * KS) {  // every k-step complete: branch-free loads
+            const int64_t rr = ok ? row : M - 1;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) x[ks] = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
+            for (int ks = 0; ks < KS; ++ks) x[ks] = x_frag_f32_full(obs, rr, ok, D, 16 * ks + 8 * h);
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) x[ks] = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
+        }
         if (xb != nullptr && ok) {
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x[ks];
@@ -481,16 +481,9 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_policy_train(TrainArgs A)
     const bool on = row0 < M;  // wave-uniform
     {
         bf8 h1[kMT][2], h2[kMT][2];
-        auto xf = [&](int ks) {
-            bf8 x;
-            if (ok) {
-                x = *reinterpret_cast<const bf8*>(A.xb + row * A.xb_stride + 16 * ks + 8 * h);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) x[j] = (__bf16)0.0f;
-            }
-            return x;
-        };
+        // branch-free: an out-of-range lane reads the last row (its results are never stored)
+        const int64_t rr = ok ? row : M - 1;
+        auto xf = [&](int ks) { return *reinterpret_cast<const bf8*>(A.xb + rr * A.xb_stride + 16 * ks + 8 * h); };
         if constexpr (KS > 0) {
             bf8 x[KS];
 #pragma unroll
@@ -656,7 +649,7 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
                       uint64_t seed, uint64_t step, int8_t* act, float* logp, float* value, hipStream_t s)
 {
     const int ks1 = (D + 15) / 16;
-    auto k = !MAS_POL_KS ? pol::k_policy_act<0> : ks1 == 10 ? pol::k_policy_act<10> : ks1 == 9 ? pol::k_policy_act<9> : pol::k_policy_act<0>;
+    auto k = ks1 == 10 ? pol::k_policy_act<10> : ks1 == 9 ? pol::k_policy_act<9> : pol::k_policy_act<0>;
     hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
                        ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, act, logp, value);
     return hipGetLastError();
@@ -687,7 +680,7 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     A.da2 = (__bf16*)da2;
     A.dz = (__bf16*)dz;
     A.partials = partials;
-    auto k = !MAS_POL_KS ? pol::k_policy_train<0> : A.ks1 == 10 ? pol::k_policy_train<10> : A.ks1 == 9 ? pol::k_policy_train<9> : pol::k_policy_train<0>;
+    auto k = A.ks1 == 10 ? pol::k_policy_train<10> : A.ks1 == 9 ? pol::k_policy_train<9> : pol::k_policy_train<0>;
     hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, A);
     return hipGetLastError();
 }

@@ -3,7 +3,9 @@ from the profiling build (libmas_prof.so, `make -C gym-ma-survival-2d_amd/csrc
 prof`).  Marks: mas_kernels.inc / mas_physics.h MAS_PROF; the first active
 lane of each wave adds the 100 MHz constant-clock time since the previous
 mark.  Prints the mean per ACTIVE wave per step (us).
-usage: python profiles/prof_general.py [n_envs] [steps]"""
+With --ppo the env is driven by the PPO trainer (2 warm-up iterations,
+then rollout steps of the trained policy): the regime of the headline bench.
+usage: python profiles/prof_general.py [n_envs] [steps] [--ppo]"""
 import ctypes
 import os
 import sys
@@ -21,14 +23,28 @@ TOI = {20: 'toi: load + sweep', 21: 'toi: reject pre-tests', 22: 'toi: b2TimeOfI
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    n = int(args[0]) if len(args) > 0 else 65536
+    steps = int(args[1]) if len(args) > 1 else 20
     lib = abi.load_library(os.path.join(os.path.dirname(abi.LIB_PATH), 'libmas_prof.so'))
     lib.mas_prof_read.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
     from masurvival.config import NAMED_CONFIGS
     from masurvival.vec_env import VecMaSurvival
     env = VecMaSurvival(NAMED_CONFIGS['2v2'], n_envs=n, auto_reset=True)
     buf = (ctypes.c_ulonglong * 64)()
+    if '--ppo' in sys.argv:
+        from masurvival.ppo import PPOConfig, PPOTrainer
+        tr = PPOTrainer(env, PPOConfig(), seed=0)
+        for _ in range(2):
+            tr.iteration()
+        abi.check(lib.mas_prof_read(env._h, buf))
+        gen_envs = 0
+        for t in range(steps):
+            tr.rollout_step(t)
+            gen_envs += env.debug_counters()['phys_general_envs']
+        abi.check(lib.mas_prof_read(env._h, buf))
+        report(buf, gen_envs, steps)
+        return
     env.reset()
     gen = torch.Generator(device=env.device)
     gen.manual_seed(0)
@@ -42,6 +58,10 @@ def main():
         env.step(acts())
         gen_envs += env.debug_counters()['phys_general_envs']
     abi.check(lib.mas_prof_read(env._h, buf))
+    report(buf, gen_envs, steps)
+
+
+def report(buf, gen_envs, steps):
     g = gen_envs / steps
     ws, wt = 2 * (g + 63) // 64, 2 * (4 * g + 63) // 64  # active waves per step (2 world steps)
     print(f'# general-path envs per step {g:.0f}; active waves per step: solve {ws:.0f}, toi {wt:.0f}')

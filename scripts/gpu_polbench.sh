@@ -4,5 +4,5 @@ O=$R/gpurun_out/polbench
 mkdir -p $O
 cd $R
 L=gym-ma-survival-2d_amd/masurvival/_lib
-timeout -k 10 300 python scripts/policy_bench.py $L/libmas_none.so $L/libmas_none.so $L/libmas_ig0.so $L/libmas_ig1.so > $O/polbench.log 2>&1 || exit $?
+timeout -k 10 300 python scripts/policy_bench.py $L/libmas_old.so $L/libmas_old.so $L/libmas_dma.so $L/libmas_old.so $L/libmas_dma.so > $O/polbench.log 2>&1 || exit $?
 echo ok
