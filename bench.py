@@ -81,9 +81,16 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # MAS_DIST_BACKEND=gloo and several ranks per GPU (local % devices) only
+    # to rehearse the multi-rank path on a one-GPU box; the real run is RCCL
+    backend = os.environ.get('MAS_DIST_BACKEND', 'nccl')
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
 
     if args.lib:
         from masurvival import abi
