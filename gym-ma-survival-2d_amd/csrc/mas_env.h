@@ -110,12 +110,14 @@ MAS_HD T sel(const T (&a)[N], int i)
     for (int k = 1; k < N; ++k) r = (i == k) ? opq(a[k]) : r;
     return r;
 }
+// every element is re-selected behind opq(): LLVM would otherwise fold the
+// unrolled compare-and-store into one store at a runtime index and demote
+// the whole array to scratch (each later read a memory round trip)
 template <int N, class T>
 MAS_HD void put(T (&a)[N], int i, T v)
 {
 #pragma unroll
-    for (int k = 0; k < N; ++k)
-        if (i == k) a[k] = v;
+    for (int k = 0; k < N; ++k) a[k] = opq(i == k ? v : a[k]);
 }
 
 template <int N, int M, class T>

@@ -451,8 +451,7 @@ __device__ __forceinline__ void spawn_heal(EnvL<C>& L, V2 pos)
     int n = L.nheal;
     if (n >= C::HM) return;
 #pragma unroll
-    for (int h = 0; h < C::HM; ++h)
-        if (h == n) L.hp[h] = pos;
+    for (int h = 0; h < C::HM; ++h) L.hp[h] = opq(h == n ? pos : L.hp[h]);  // selects, see put()
     L.nheal = n + 1;
 }
 

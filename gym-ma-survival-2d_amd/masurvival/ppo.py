@@ -21,6 +21,7 @@ group is 'nccl', gloo in the CPU tests.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -54,7 +55,7 @@ class PPOConfig:
     fused: Optional[bool] = None
 
 
-def _split_k(m: int, cap: int = 64) -> int:
+def _split_k(m: int, cap: int = int(os.environ.get('MAS_SPLITK_CAP', '64'))) -> int:
     c = 1
     while c < cap and m % (2 * c) == 0 and m // (2 * c) >= 4096:
         c *= 2
