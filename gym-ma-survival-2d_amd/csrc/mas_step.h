@@ -101,20 +101,22 @@ __device__ __forceinline__ int ray_cast(const EnvL<C>& L, const Params& P, V2 p1
 // Fixture table: per-lane LDS copy of what a ray test needs by runtime body
 // index (positions of every body, box half-extents + meta), [field][kWG]
 // interleaved so a wave's 64 lanes hit 64 distinct banks.
-template <class C>
+template <class C, int S = kWG>  // S: tables in the block ([field][S] interleaved)
 struct FixTab {
-    float* f;  // [2*NB + 3*BM][kWG]
-    int tid;
-    static constexpr int kWords = 2 * C::NB + 3 * C::BM;
-    __device__ float& px(int k) const { return f[k * kWG + tid]; }
-    __device__ float& py(int k) const { return f[(C::NB + k) * kWG + tid]; }
-    __device__ float& hx(int b) const { return f[(2 * C::NB + b) * kWG + tid]; }
-    __device__ float& hy(int b) const { return f[(2 * C::NB + C::BM + b) * kWG + tid]; }
-    __device__ float& meta(int b) const { return f[(2 * C::NB + 2 * C::BM + b) * kWG + tid]; }
+    float* f;  // [2*NB + 3*BM + 1][S]
+    int tid;   // this table's column
+    static constexpr int kWords = 2 * C::NB + 3 * C::BM + 1;
+    __device__ float& px(int k) const { return f[k * S + tid]; }
+    __device__ float& py(int k) const { return f[(C::NB + k) * S + tid]; }
+    __device__ float& hx(int b) const { return f[(2 * C::NB + b) * S + tid]; }
+    __device__ float& hy(int b) const { return f[(2 * C::NB + C::BM + b) * S + tid]; }
+    __device__ float& meta(int b) const { return f[(2 * C::NB + 2 * C::BM + b) * S + tid]; }
+    // nbox | nbi << 8 | nheal << 16 | alive mask << 24
+    __device__ float& counts() const { return f[(2 * C::NB + 3 * C::BM) * S + tid]; }
 };
 
-template <class C>
-__device__ __forceinline__ void build_fixtab(const EnvL<C>& L, const Params& P, const FixTab<C>& T)
+template <class C, int S>
+__device__ __forceinline__ void build_fixtab(const EnvL<C>& L, const Params& P, const FixTab<C, S>& T)
 {
 #pragma unroll
     for (int b = 0; b < C::BM; ++b) {
@@ -141,6 +143,7 @@ __device__ __forceinline__ void build_fixtab(const EnvL<C>& L, const Params& P, 
         T.px(BIdx<C>::agent + i) = L.c[i].x;
         T.py(BIdx<C>::agent + i) = L.c[i].y;
     }
+    T.counts() = __int_as_float(L.nbox | (L.nbi << 8) | (L.nheal << 16) | (int)(L.alive_m << 24));
 }
 
 // ray_cast with Box2D's own broadphase test in front: b2DynamicTree::RayCast
@@ -222,6 +225,86 @@ __device__ __forceinline__ int ray_cast_tab(const EnvL<C>& L, const Params& P, c
     return hit;
 }
 
+// ray_cast_tab with every input read from a fixture table (the env of any
+// lane of the block): the same broadphase cull and the same exact tests in
+// the same canonical order, so the same first hit
+template <class C, int S>
+__device__ __forceinline__ int ray_cast_fixtab(const Params& P, const FixTab<C, S>& T, V2 p1, V2 p2)
+{
+    constexpr float m = 1e-3f;
+    const V2 r = sub(p2, p1);
+    const float rl = len(r);
+    const V2 rn = rl > 0.0f ? scl(1.0f / rl, r) : mk(0.0f, 0.0f);
+    const V2 v = mk(-rn.y, rn.x);
+    const V2 av = mk(fabsf(v.x), fabsf(v.y));
+    const float lox = fminf(p1.x, p2.x) - m, loy = fminf(p1.y, p2.y) - m;
+    const float hix = fmaxf(p1.x, p2.x) + m, hiy = fmaxf(p1.y, p2.y) + m;
+    auto keep = [&](V2 c, float ex, float ey) -> bool {
+        if (c.x - ex > hix || c.x + ex < lox || c.y - ey > hiy || c.y + ey < loy) return false;
+        return fabsf(dot(v, sub(p1, c))) - (av.x * ex + av.y * ey) <= m;
+    };
+    const int cnt = __float_as_int(T.counts());
+    const int nbox = cnt & 0xff, nbi = (cnt >> 8) & 0xff, nheal = (cnt >> 16) & 0xff;
+    const uint32_t alive = (uint32_t)cnt >> 24;
+    uint64_t mask = 0;
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (b < nbox && keep(mk(T.px(BIdx<C>::box + b), T.py(BIdx<C>::box + b)), T.hx(b), T.hy(b)))
+            mask |= 1ull << (BIdx<C>::box + b);
+        if (b < nbi && keep(mk(T.px(BIdx<C>::bitem + b), T.py(BIdx<C>::bitem + b)), P.bitem_r, P.bitem_r))
+            mask |= 1ull << (BIdx<C>::bitem + b);
+    }
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h)
+        if (h < nheal && keep(mk(T.px(BIdx<C>::heal + h), T.py(BIdx<C>::heal + h)), P.heal_r, P.heal_r))
+            mask |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+    for (int w = 0; w < kNumWalls; ++w) {
+        V2 c = scl(0.5f, add(P.wall_lo[w], P.wall_hi[w]));
+        V2 e = scl(0.5f, sub(P.wall_hi[w], P.wall_lo[w]));
+        if (keep(c, e.x + m, e.y + m)) mask |= 1ull << (BIdx<C>::wall + w);
+    }
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i)
+        if (bit(alive, i) && keep(mk(T.px(BIdx<C>::agent + i), T.py(BIdx<C>::agent + i)), P.agent_r, P.agent_r))
+            mask |= 1ull << (BIdx<C>::agent + i);
+
+    float maxf = 1.0f;
+    int hit = -1;
+    while (mask) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const V2 c = mk(T.px(k), T.py(k));
+        float f;
+        const bool is_box = k < BIdx<C>::bitem;
+        const bool is_wall = k >= BIdx<C>::wall && k < BIdx<C>::agent;
+        if (is_box || is_wall) {
+            Poly4 poly;
+            Rot q = kIdRot;
+            if (is_box) {
+                const int meta = __float_as_int(T.meta(k));
+                poly = box_poly(T.hx(k), T.hy(k), box_rot(meta), box_copied(meta));
+            } else {
+                poly = P.wall_poly;
+                const int w = k - BIdx<C>::wall;
+#pragma unroll
+                for (int q2 = 0; q2 < kNumWalls; ++q2)
+                    if (q2 == w) { q.s = opq(P.wall_q[q2].s); q.c = opq(P.wall_q[q2].c); }
+            }
+            f = ray_poly(poly, c, q, p1, p2, maxf);
+        } else {
+            const float rad = k < BIdx<C>::heal ? P.bitem_r : (k < BIdx<C>::wall ? P.heal_r : P.agent_r);
+            f = ray_circle(rad, c, p1, p2, maxf);
+        }
+        if (f >= 0.0f) {
+            hit = k;
+            maxf = f;
+            if (maxf == 0.0f) break;
+        }
+    }
+    return hit;
+}
+
 // Cameras._update_seen (simulation.py:336-354): camera list position p =
 // rank among the alive agents; scr.sn(body) gets bit p when body is in the
 // vision cone and the LOS ray to pos + (1+1e-6)*d hits it first.  All
@@ -270,49 +353,79 @@ __device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, S
 }
 
 // update_seen for the single camera slot `cam` (k_cameras runs one lane per
-// (env, camera) and ORs the lanes' masks): same candidate order and rays as
-// update_seen restricted to camera cam, whose camera-list position is its
-// rank among the alive agents.
+// (env, camera) and ORs the lanes' masks).  Each lane's cone query appends
+// its (camera position, lane, body) candidates to the wave's list in LDS; the
+// line-of-sight rays of the whole wave are then dealt round-robin over its
+// 64 lanes (each ray reads the owner lane's fixture table), so a wave costs
+// its mean candidate count, not its maximum.  Same candidates, same rays,
+// same first-hit test: the seen masks are unchanged.  One fixture table and
+// one seen row per env of the wave (column = env slot = lane / AM); the seen
+// row must be zero on entry; `list` holds kWG * NB entries; the block is one
+// wave.
 template <class C>
-__device__ __forceinline__ void update_seen_cam(const EnvL<C>& L, const Params& P, Scr<C>& scr, const FixTab<C>& T,
-                                                int cam)
+__device__ __forceinline__ void update_seen_cam(const EnvL<C>& L, const Params& P, uint32_t* seen,
+                                                const FixTab<C, kWG / C::AM>& T, int cam, uint32_t* list, bool active)
 {
-#pragma unroll
-    for (int k = 0; k < C::NB; ++k) scr.sn(k) = 0u;
-    if (!bit(L.alive_m, cam)) return;
-    const int p = __popc(L.alive_m & ((1u << cam) - 1u));
+    const int lane = (int)threadIdx.x & 63;
+    static_assert(C::NB <= 64, "body bit masks are 64-bit");
+    uint64_t cand = 0;  // bit per body in the cone
+    int p = 0;
     V2 pos = mk(0.0f, 0.0f);
-    float ang = 0.0f;
+    if (active && bit(L.alive_m, cam)) {
+        p = __popc(L.alive_m & ((1u << cam) - 1u));
+        float ang = 0.0f;
 #pragma unroll
-    for (int i = 0; i < C::AM; ++i)
-        if (i == cam) { pos = opq(L.c[i]); ang = opq(L.a[i]); }
-    const Rot q = rot_of(ang);
-    int np = 0;
+        for (int i = 0; i < C::AM; ++i)
+            if (i == cam) { pos = opq(L.c[i]); ang = opq(L.a[i]); }
+        const Rot q = rot_of(ang);
 #pragma unroll
-    for (int b = 0; b < C::BM; ++b)
-        if (b < L.nbox && poly_test_point(P.cone, pos, q, L.bp[b])) scr.pr(np++) = BIdx<C>::box + b;
+        for (int b = 0; b < C::BM; ++b)
+            if (b < L.nbox && poly_test_point(P.cone, pos, q, L.bp[b])) cand |= 1ull << (BIdx<C>::box + b);
 #pragma unroll
-    for (int b = 0; b < C::BM; ++b)
-        if (b < L.nbi && poly_test_point(P.cone, pos, q, L.ip[b])) scr.pr(np++) = BIdx<C>::bitem + b;
+        for (int b = 0; b < C::BM; ++b)
+            if (b < L.nbi && poly_test_point(P.cone, pos, q, L.ip[b])) cand |= 1ull << (BIdx<C>::bitem + b);
 #pragma unroll
-    for (int h = 0; h < C::HM; ++h)
-        if (h < L.nheal && poly_test_point(P.cone, pos, q, L.hp[h])) scr.pr(np++) = BIdx<C>::heal + h;
+        for (int h = 0; h < C::HM; ++h)
+            if (h < L.nheal && poly_test_point(P.cone, pos, q, L.hp[h])) cand |= 1ull << (BIdx<C>::heal + h);
 #pragma unroll
-    for (int w = 0; w < kNumWalls; ++w)
-        if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) scr.pr(np++) = BIdx<C>::wall + w;
+        for (int w = 0; w < kNumWalls; ++w)
+            if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) cand |= 1ull << (BIdx<C>::wall + w);
 #pragma unroll
-    for (int j = 0; j < C::AM; ++j)
-        if (j != cam && bit(L.alive_m, j) && poly_test_point(P.cone, pos, q, L.c[j]))
-            scr.pr(np++) = BIdx<C>::agent + j;
-    MAS_PROF(P, 13);
-    const float eps1 = (float)(1.0 + 1e-6);
-    for (int t = 0; t < np; ++t) {
-        const int body = (int)scr.pr(t);
-        const V2 oc = mk(T.px(body), T.py(body));
-        const V2 d = sub(oc, pos);
-        const V2 end = add(pos, scl(eps1, d));
-        if (ray_cast_tab(L, P, T, pos, end) == body) scr.sn(body) |= 1u << p;
+        for (int j = 0; j < C::AM; ++j)
+            if (j != cam && bit(L.alive_m, j) && poly_test_point(P.cone, pos, q, L.c[j]))
+                cand |= 1ull << (BIdx<C>::agent + j);
     }
+    MAS_PROF(P, 13);
+    // wave prefix sum of the candidate counts
+    const int np = __popcll(cand);
+    int incl = np;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int total = __shfl(incl, 63, 64);
+    int at = incl - np;
+    while (cand) {
+        const int body = __builtin_ctzll(cand);
+        cand &= cand - 1;
+        list[at++] = ((uint32_t)p << 16) | ((uint32_t)lane << 8) | (uint32_t)body;
+    }
+    __syncthreads();  // the block is this wave: the list and every fixture table are visible
+    constexpr int S = kWG / C::AM;
+    const float eps1 = (float)(1.0 + 1e-6);
+    for (int j = lane; j < total; j += 64) {
+        const uint32_t en = list[j];
+        const int body = (int)(en & 0xffu), o = (int)((en >> 8) & 0xffu), pc = (int)(en >> 16);
+        const FixTab<C, S> To{T.f, o / C::AM};
+        const int ocam = o % C::AM;  // the owner lane's camera slot
+        const V2 opos = mk(To.px(BIdx<C>::agent + ocam), To.py(BIdx<C>::agent + ocam));
+        const V2 oc = mk(To.px(body), To.py(body));
+        const V2 d = sub(oc, opos);
+        const V2 end = add(opos, scl(eps1, d));
+        if (ray_cast_fixtab(P, To, opos, end) == body) atomicOr(&seen[body * S + o / C::AM], 1u << pc);
+    }
+    __syncthreads();
 }
 
 // Cameras.seen <-> state bytes (kGSeen): byte k = camera-position mask of body k
