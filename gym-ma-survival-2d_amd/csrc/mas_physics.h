@@ -617,13 +617,31 @@ struct ToiPoly {
     Poly4 P;
     V2 c;  // static position (c0 == c)
     float ang;
+    Rot q0;  // rot_of(ang)
 };
 
+MAS_HD ToiPoly toi_poly(const Poly4& P, V2 c, float ang)
+{
+    ToiPoly T;
+    T.P = P;
+    T.c = c;
+    T.ang = ang;
+    T.q0 = rot_of(ang);
+    return T;
+}
+
+// b2Sweep::GetTransform of the static: the interpolated angle is almost
+// always bit-identical to ang (always for ang = 0), and then its rotation is
+// q0 -- the same rot_of of the same bits, without the fp64 sincos
 MAS_HD void sweep_static(const ToiPoly& T, float beta, V2& p, Rot& q)
 {
     p = add(scl(1.0f - beta, T.c), scl(beta, T.c));
     float angle = (1.0f - beta) * T.ang + beta * T.ang;
-    q = rot_of(angle);
+    uint32_t ua, ub;
+    memcpy(&ua, &angle, 4);
+    memcpy(&ub, &T.ang, 4);
+    if (ua == ub) q = T.q0;
+    else q = rot_of(angle);
 }
 
 MAS_HD V2 sweep_point(const Sweep& B, float beta)
@@ -1026,6 +1044,17 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
 #pragma unroll
     for (int s = 0; s < C::NS; ++s) { toi[s] = 1.0f; cnt[s] = 0; }
     uint32_t valid = 0, enabled = 0xffffffffu;
+#ifdef MAS_PROFILE
+    unsigned long long nev = 0, ntoi = 0, npos = 0, lt = wall_clock64(), tp[5] = {0, 0, 0, 0, 0};
+#define MAS_LT(k)                                 \
+    do {                                          \
+        const unsigned long long n_ = wall_clock64(); \
+        tp[k] += n_ - lt;                         \
+        lt = n_;                                  \
+    } while (0)
+#else
+#define MAS_LT(k) ((void)0)
+#endif
     for (int guard = 0; guard < 9 * C::NS + 1; ++guard) {
         // (1) statics whose cached TOI is stale: the conservative pre-test
         //     settles most of them at alpha = 1 (unrolled, cheap)
@@ -1042,17 +1071,18 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
             }
         }
         MAS_PROF(P, 21);
+        MAS_LT(0);
         // (2) full b2TimeOfImpact for the rest (runtime loop: one code copy)
 #pragma unroll 1
         while (need) {
             int s = __builtin_ctz(need);
             need &= need - 1;
             StaticG g = static_geom_dyn(L, P, s);
-            ToiPoly T;
-            T.P = g.poly;
-            T.c = g.p;
-            T.ang = g.angle;
+            const ToiPoly T = toi_poly(g.poly, g.p, g.angle);
             float beta;
+#ifdef MAS_PROFILE
+            ++ntoi;
+#endif
             int st = time_of_impact(T, sw, P.agent_r, beta);
             float alpha = 1.0f;
             if (st == kToiTouching) alpha = fmin_b2(sw.alpha0 + (1.0f - sw.alpha0) * beta, 1.0f);
@@ -1060,6 +1090,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
             valid |= 1u << s;
         }
         MAS_PROF(P, 22);
+        MAS_LT(1);
         // (3) minimum over the enabled contacts (ties: lowest canonical index)
         float minAlpha = 1.0f;
         int minS = -1;
@@ -1072,6 +1103,9 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
             }
         }
         if (minS < 0 || 1.0f - 10.0f * kEps < minAlpha) break;
+#ifdef MAS_PROFILE
+        ++nev;
+#endif
         Sweep backup = sw;
         {
             float beta = (minAlpha - sw.alpha0) / (1.0f - sw.alpha0);
@@ -1110,10 +1144,14 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
             StaticG g = static_geom(L, P, s);
             if (update_as_g(L, P, K, I, s, g, iln[s], ilp[s])) isl |= 1u << s;
         }
+        MAS_LT(2);
         // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
         V2 cB = sel(L.c, I);
         float aB = sel(L.a, I);
         for (int it = 0; it < 20; ++it) {
+#ifdef MAS_PROFILE
+            ++npos;
+#endif
             float minsep = 0.0f;
             minsep = fmin_b2(minsep, pc_solve_as(gm.p, gm.q, lnm, lpm, cB, aB, P.agent_r, m, Ii, kToiBaumgarte));
 #pragma unroll
@@ -1124,6 +1162,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
             }
             if (minsep >= -1.5f * kLinearSlop) break;
         }
+        MAS_LT(3);
         sw.c0 = cB;
         sw.a0 = aB;
         // ... then 10 velocity iterations without warm starting
@@ -1168,9 +1207,21 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
         sw.a = aB;
         valid = 0;
         MAS_PROF(P, 24);
+        MAS_LT(4);
     }
     put(L.c, I, sw.c);
     put(L.a, I, sw.a);
+#ifdef MAS_PROFILE
+    // per-lane SolveTOI work: max events / b2TimeOfImpact calls / position
+    // iterations over the launch's lanes, and the event total
+    atomicMax(&P.prof[48], nev);
+    atomicMax(&P.prof[49], ntoi);
+    atomicMax(&P.prof[50], npos);
+    atomicAdd(&P.prof[51], nev);
+    atomicAdd(&P.prof[52], ntoi);
+    for (int k = 0; k < 5; ++k) atomicMax(&P.prof[53 + k], tp[k]);
+#endif
+#undef MAS_LT
 }
 
 

@@ -139,6 +139,9 @@ __global__ void k_pack(int D, int ks1, const float* __restrict__ W1, const float
 }
 
 // timing experiments only (results garbage): 1 no tanh, 2 no sampling, 4 no MFMA, 8 no x loads
+#ifndef MAS_POL_OCC_ACT
+#define MAS_POL_OCC_ACT 2
+#endif
 #ifndef MAS_POL_EXP
 #define MAS_POL_EXP 0
 #endif
@@ -359,7 +362,7 @@ constexpr int kHeadOff[6] = {0, 3, 6, 9, 11, 13};
 // KS > 0: compile-time k-step count (obs_dim in (16 (KS-1), 16 KS]) with every
 // x fragment loaded up front; KS == 0: any obs_dim, chunked layer 1
 template <int KS>
-__global__ __launch_bounds__(64 * kWaves, 2) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
+__global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
                                                              int64_t M, const float* __restrict__ obs,
                                                              __bf16* __restrict__ xb, int64_t xb_stride,
                                                              uint64_t seed, uint64_t step, int8_t* __restrict__ act,
@@ -465,8 +468,73 @@ struct TrainArgs {
     float* partials;        // [gridDim.x][4]: sum pg, sum (v-ret)^2, sum entropy, clipped count
 };
 
+// Feature-major activation store of one 32-row M-tile fragment (16 features
+// crow(i, h) of 32*mt.. for this lane's row).  Lanes l and l^1 hold rows r and
+// r^1 of the same features: one DPP swap per feature pair lets each lane write
+// two consecutive rows of one feature as a 4-B word (half the store
+// instructions of 2-B stores, full 128-B segments per wave half).  Needs M even
+// (then both rows of a pair are in range or neither is).
+// MAS_POL_PAIR: rows per lane of the feature-major stores when M allows (1, 2, 4)
+#ifndef MAS_POL_PAIR
+#define MAS_POL_PAIR 2
+#endif
+// waves per SIMD of the train kernel (A/B: 1 = 512 registers, no spills)
+#ifndef MAS_POL_OCC
+#define MAS_POL_OCC 2
+#endif
+__device__ __forceinline__ void store_rows2(__bf16* base, int64_t M, int64_t row, int mt, int h, const bf8 (&v)[2])
+{
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const bool odd = row & 1;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(base + (row & ~(int64_t)1));
+    const u4 w[2] = {__builtin_bit_cast(u4, v[0]), __builtin_bit_cast(u4, v[1])};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        // features 2j (low half) and 2j + 1 (high half) of this lane's row
+        const uint32_t a = w[j >> 2][j & 3] & 0xffffu, b = w[j >> 2][j & 3] >> 16;
+        // quad_perm [1, 0, 3, 2]: lane l reads lane l ^ 1
+        const uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? a : b), 0xB1, 0xF, 0xF, false) & 0xffffu;
+        const uint32_t word = odd ? (r | (b << 16)) : (a | (r << 16));
+        const int64_t f = 32 * mt + crow(odd ? 2 * j + 1 : 2 * j, h);
+        dst[(f * M) >> 1] = word;
+    }
+}
+
+// Same with four consecutive rows per lane (8-B stores): a 4 x 4 transpose of
+// bf16 within each lane quad (rows r..r+3 x features crow(4g..4g+3)) in two
+// DPP exchanges, after which lane q of the quad holds feature 4g + q of all
+// four rows.  Needs M % 4 == 0.
+__device__ __forceinline__ void store_rows4(__bf16* base, int64_t M, int64_t row, int mt, int h, const bf8 (&v)[2])
+{
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const int q = (int)(row & 3);
+    const bool hi = q & 2, odd = q & 1;
+    const u4 w[2] = {__builtin_bit_cast(u4, v[0]), __builtin_bit_cast(u4, v[1])};
+    uint2* dst = reinterpret_cast<uint2*>(base + (row & ~(int64_t)3));
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const uint32_t W0 = w[g >> 1][2 * (g & 1)], W1 = w[g >> 1][2 * (g & 1) + 1];  // features 4g+0,1 / 4g+2,3
+        // quad_perm [2, 3, 0, 1]: rows q and q ^ 2 trade the feature pair the other keeps
+        const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)(hi ? W0 : W1), 0x4E, 0xF, 0xF, false);
+        const uint32_t X = hi ? r1 : W0, Y = hi ? W1 : r1;  // rows (q & 1), (q & 1) + 2 of feature pair (q & 2)
+        const uint32_t s2 = odd ? ((X & 0xffffu) | (Y << 16)) : ((X >> 16) | (Y & 0xffff0000u));
+        // quad_perm [1, 0, 3, 2]: rows q and q ^ 1 trade halves
+        const uint32_t r2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s2, 0xB1, 0xF, 0xF, false);
+        uint2 o;
+        if (odd) {
+            o.x = (r2 & 0xffffu) | (X & 0xffff0000u);
+            o.y = (r2 >> 16) | (Y & 0xffff0000u);
+        } else {
+            o.x = (X & 0xffffu) | (r2 << 16);
+            o.y = (Y & 0xffffu) | (r2 & 0xffff0000u);
+        }
+        const int64_t f = 32 * mt + 8 * g + 4 * h + q;  // crow(4g + q, h)
+        dst[(f * M) >> 2] = o;
+    }
+}
+
 template <int KS>
-__global__ __launch_bounds__(64 * kWaves, 2) void k_policy_train(TrainArgs A)
+__global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC) void k_policy_train(TrainArgs A)
 {
     __shared__ bf8 wl[kLdsFrag];
     const Layout Lo{A.ks1};
@@ -495,15 +563,30 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_policy_train(TrainArgs A)
         const f16v z3 = layers23<true>(wl, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);
         stage(wl, F + Lo.wbk(), kBk0 * 64);  // W3^T
         // feature-major activations for the weight gradients
+        // wave-uniform store mode: 4 rows per lane (M % 4 == 0), 2 rows (M even), 1 row
+        const int rows_per_lane = !MAS_POL_PAIR ? 1 : (M & 3) == 0 ? MAS_POL_PAIR : (M & 1) == 0 ? 2 : 1;
+        const bool pair = rows_per_lane > 1;
+        auto store_rows = [&](__bf16* base, int t, const bf8 (&v)[2]) {
+            if (rows_per_lane == 4) store_rows4(base, M, row, t, h, v);
+            else store_rows2(base, M, row, t, h, v);
+        };
         if (on && ok) {
+            if (pair) {
 #pragma unroll
-            for (int mt = 0; mt < kMT; ++mt)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int64_t f = 32 * mt + crow(i, h);
-                    A.h1[f * M + row] = h1[mt][i >> 3][i & 7];
-                    A.h2[f * M + row] = h2[mt][i >> 3][i & 7];
+                for (int mt = 0; mt < kMT; ++mt) {
+                    store_rows(A.h1, mt, h1[mt]);
+                    store_rows(A.h2, mt, h2[mt]);
                 }
+            } else {
+#pragma unroll
+                for (int mt = 0; mt < kMT; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int64_t f = 32 * mt + crow(i, h);
+                        A.h1[f * M + row] = h1[mt][i >> 3][i & 7];
+                        A.h2[f * M + row] = h2[mt][i >> 3][i & 7];
+                    }
+            }
         }
         // PPO loss gradient of this row (lane half 0 holds the 16 outputs)
         float dz[kO];
@@ -585,8 +668,12 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_policy_train(TrainArgs A)
                 da2[mo][i >> 3][i & 7] = (__bf16)(g[i] * (1.0f - hv * hv));
             }
             if (ok) {
+                if (pair) {
+                    store_rows(A.da2, mo, da2[mo]);
+                } else {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) A.da2[(int64_t)(32 * mo + crow(i, h)) * M + row] = da2[mo][i >> 3][i & 7];
+                    for (int i = 0; i < 16; ++i) A.da2[(int64_t)(32 * mo + crow(i, h)) * M + row] = da2[mo][i >> 3][i & 7];
+                }
             }
         }
         // dA1 = (W2^T dA2) * (1 - h1^2), by M-tile of layer 1
@@ -599,10 +686,17 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_policy_train(TrainArgs A)
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk) g = mfma(W2T[((mt % (kMT / 2)) * 16 + kk) * 64], da2[kk >> 1][kk & 1], g);
             if (ok) {
+                bf8 d1[2];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const float hv = (float)h1[mt][i >> 3][i & 7];
-                    A.da1[(int64_t)(32 * mt + crow(i, h)) * M + row] = (__bf16)(g[i] * (1.0f - hv * hv));
+                    d1[i >> 3][i & 7] = (__bf16)(g[i] * (1.0f - hv * hv));
+                }
+                if (pair) {
+                    store_rows(A.da1, mt, d1);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) A.da1[(int64_t)(32 * mt + crow(i, h)) * M + row] = d1[i >> 3][i & 7];
                 }
             }
         }

@@ -1,6 +1,6 @@
 """Time the pieces of one PPO rollout step and of the update separately
 (HIP events on the current stream): policy forward + sample, env step,
-finish_rollout (GAE), update.  usage: python scripts/ppo_breakdown.py [n_envs]"""
+finish_rollout (GAE), update.  usage: python scripts/ppo_breakdown.py [n_envs] [iterations]"""
 import os
 import sys
 import time
@@ -35,7 +35,8 @@ def main():
         marks.append((e1, e2))
         return r
     env.step = timed_step
-    for it in range(3):
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    for it in range(iters):
         marks.clear()
         e0 = ev(); e0.record()
         starts = []
@@ -53,7 +54,8 @@ def main():
         print(f'iter {it}: rollout {e0.elapsed_time(e_roll):.2f} ms (policy fwd+sample {pol_ms:.2f}, env {env_ms:.2f}), '
               f'finish {e_roll.elapsed_time(e_fin):.2f} ms, update {e_fin.elapsed_time(e_upd):.2f} ms; '
               f'per step: policy {pol_ms / T:.3f} env {env_ms / T:.3f} update+finish '
-              f'{e_roll.elapsed_time(e_upd) / T:.3f} ms', flush=True)
+              f'{e_roll.elapsed_time(e_upd) / T:.3f} ms; env step max {max(a.elapsed_time(b) for a, b in marks):.3f} ms, '
+              f'general envs {env.debug_counters()["phys_general_envs"]}', flush=True)
 
 
 if __name__ == '__main__':
