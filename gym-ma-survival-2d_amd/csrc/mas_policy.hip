@@ -40,7 +40,10 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 constexpr int kH = 256;   // hidden width
 constexpr int kMT = 8;    // 32-row M-tiles of a hidden layer
 constexpr int kO = 16;    // real outputs of layer 3 (15 logits + value)
-constexpr int kWaves = 4; // waves per workgroup (one per SIMD; two workgroups per CU)
+#ifndef MAS_POL_WAVES
+#define MAS_POL_WAVES 4
+#endif
+constexpr int kWaves = MAS_POL_WAVES;  // waves per workgroup (4: one per SIMD, two workgroups per CU)
 constexpr int kLdsFrag = 4608;  // 72 KiB LDS weight stage (16-B fragments): two workgroups per CU
 constexpr int kKc = kLdsFrag / (kMT * 64);  // layer-1 k-steps per stage (9)
 constexpr int kHalf = kMT / 2 * 16 + 8;     // fragment slots of one forward half stage: W2 4 M-tiles + W3 8 k-steps
@@ -362,7 +365,7 @@ constexpr int kHeadOff[6] = {0, 3, 6, 9, 11, 13};
 // KS > 0: compile-time k-step count (obs_dim in (16 (KS-1), 16 KS]) with every
 // x fragment loaded up front; KS == 0: any obs_dim, chunked layer 1
 template <int KS>
-__global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
+__global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
                                                              int64_t M, const float* __restrict__ obs,
                                                              __bf16* __restrict__ xb, int64_t xb_stride,
                                                              uint64_t seed, uint64_t step, int8_t* __restrict__ act,
@@ -534,7 +537,7 @@ __device__ __forceinline__ void store_rows4(__bf16* base, int64_t M, int64_t row
 }
 
 template <int KS>
-__global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC) void k_policy_train(TrainArgs A)
+__global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_policy_train(TrainArgs A)
 {
     __shared__ bf8 wl[kLdsFrag];
     const Layout Lo{A.ks1};
