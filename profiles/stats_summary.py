@@ -1,11 +1,27 @@
 """Summarise a rocprofv3 --stats kernel table (run_kernel_stats.csv) into text.
-usage: python profiles/stats_summary.py <run_kernel_stats.csv> <out.txt> "<header line>" [steps]
-With [steps], adds the per-step share (total / steps) of each kernel."""
+usage: python profiles/stats_summary.py <run_kernel_stats.csv> <out.txt> "<header line>" [steps] [trace.csv timed]
+With [steps], adds the per-step share (total / steps) of each kernel.  With
+the kernel trace and the number of timed steps, adds the duration of the env
+step's launch group (k_pre start -> k_obs end, what bench.py times with HIP
+events as `roofline.kernel_ms`) over the last `timed` steps."""
 import csv
 import sys
 
 
-def main(path, out, header, steps=None):
+def step_spans(trace):
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r['Start_Timestamp']))
+    spans, t0 = [], None
+    for r in rows:
+        n = r['Kernel_Name']
+        if 'mas::k_pre<' in n:
+            t0 = int(r['Start_Timestamp'])
+        elif 'mas::k_obs<' in n and t0 is not None:
+            spans.append((int(r['End_Timestamp']) - t0) / 1e6)
+            t0 = None
+    return spans
+
+
+def main(path, out, header, steps=None, trace=None, timed=None):
     rows = list(csv.DictReader(open(path)))
     lines = ['# ' + header, '# durations in ns; one row per kernel name (first 100 chars)',
              'name | calls | total_ns | avg_ns | min_ns | max_ns | pct' + (' | us_per_step' if steps else '')]
@@ -15,6 +31,11 @@ def main(path, out, header, steps=None):
         if steps:
             x.append('%.1f' % (float(r['TotalDurationNs']) / 1e3 / float(steps)))
         lines.append(' | '.join(x))
+    if trace:
+        sp = step_spans(trace)
+        k = int(timed)
+        lines.append('# mas_step launch group (k_pre start -> k_obs end): mean %.4f ms over the last %d steps '
+                     '(the timed region), %.4f ms over all %d steps' % (sum(sp[-k:]) / k, k, sum(sp) / len(sp), len(sp)))
     open(out, 'w').write('\n'.join(lines) + '\n')
 
 

@@ -24,6 +24,6 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_env -o run -- python3 $R/bench.py --mode env --no-cpu-baseline > $O/prof_env.log 2>&1 || exit $?
 cd $R
-python profiles/stats_summary.py $O/prof_bench/run_kernel_stats.csv profiles/${TAG}_kernel_stats.txt "round ${TAG#r}: rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline (MI355X, 2v2 N_envs=65536, PPO: 64 warmup + 128 timed steps, 3 updates)" 192 || exit $?
-python profiles/stats_summary.py $O/prof_env/run_kernel_stats.csv profiles/${TAG}_kernel_stats_env.txt "round ${TAG#r}: rocprofv3 --kernel-trace --stats -- python3 bench.py --mode env --no-cpu-baseline (MI355X, 2v2 N_envs=65536, random policy: 64 warmup + 128 timed steps)" 192 || exit $?
+python profiles/stats_summary.py $O/prof_bench/run_kernel_stats.csv profiles/${TAG}_kernel_stats.txt "round ${TAG#r}: rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline (MI355X, 2v2 N_envs=65536, PPO: 64 warmup + 128 timed steps, 3 updates)" 192 $O/prof_bench/run_kernel_trace.csv 128 || exit $?
+python profiles/stats_summary.py $O/prof_env/run_kernel_stats.csv profiles/${TAG}_kernel_stats_env.txt "round ${TAG#r}: rocprofv3 --kernel-trace --stats -- python3 bench.py --mode env --no-cpu-baseline (MI355X, 2v2 N_envs=65536, random policy: 64 warmup + 128 timed steps)" 192 $O/prof_env/run_kernel_trace.csv 128 || exit $?
 echo ok
