@@ -76,6 +76,8 @@ def main():
     ap.add_argument('--horizon', type=int, default=64)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--lib', default=None, help='alternative libmas*.so (A/B variants)')
+    ap.add_argument('--shards', type=int, default=1,
+                    help='env handles per GPU, each on its own HIP stream (vec_env.ShardedVecMaSurvival)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -99,11 +101,27 @@ def main():
     from masurvival.vec_env import VecMaSurvival
     cfg = NAMED_CONFIGS[args.config]
     n = args.envs or {'1v1': 4096, '2v2': 65536, 'ffa4': 16384}[args.config]
-    env = VecMaSurvival(cfg, n_envs=n, seeds=range(rank * n, rank * n + n), auto_reset=True)
+    if args.shards > 1:
+        from masurvival.vec_env import ShardedVecMaSurvival
+        env = ShardedVecMaSurvival(cfg, n_envs=n, shards=args.shards, seeds=range(rank * n, rank * n + n),
+                                   auto_reset=True)
+    else:
+        env = VecMaSurvival(cfg, n_envs=n, seeds=range(rank * n, rank * n + n), auto_reset=True)
     A, D = env.n_agents, env.obs_dim
     dev = env.device
     # the env kernel's launch duration, HIP events on the stream it runs on
     kev = []
+    if args.shards > 1:
+        # one mas_step launch group per shard, timed on the shard's stream
+        for sub in env.envs:
+            def timed_shard_step(a, out=None, _step=sub.step):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                r = _step(a, out=out)
+                e1.record()
+                kev.append((e0, e1))
+                return r
+            sub.step = timed_shard_step
 
     if args.mode == 'ppo':
         from masurvival.ppo import PPOConfig, PPOTrainer
@@ -118,7 +136,8 @@ def main():
             e1.record()
             kev.append((e0, e1))
             return r
-        env.step = timed_env_step
+        if args.shards == 1:
+            env.step = timed_env_step
         state = {'t': 0, 'updates': 0}
 
         def one_step():
@@ -139,6 +158,9 @@ def main():
         def one_step():
             u = torch.rand((n, A, 6), generator=gen, device=dev)
             acts.copy_((u * hi).to(torch.int8))
+            if args.shards > 1:
+                env.step(acts)
+                return
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             env.step(acts)
@@ -171,7 +193,8 @@ def main():
     diag = env.debug_counters()
     total_agent_steps = world * n * A * args.steps
     b_env = algorithmic_bytes_per_env_step(A, env.rc.n_heals, env.rc.n_boxes, D)
-    achieved = b_env * n / (kern_ms * 1e-3) / 1e9
+    n_launch = n // args.shards  # envs per mas_step launch group (per shard when sharded)
+    achieved = b_env * n_launch / (kern_ms * 1e-3) / 1e9
     workload = (f'{args.config} PPO rollout (policy MLP 2x256 bf16 fwd + sample + env step + buffer), '
                 f'GAE + PPO update (1 epoch, 4 minibatches) every {args.horizon} steps'
                 if args.mode == 'ppo' else f'{args.config} env step, random policy')
@@ -187,11 +210,14 @@ def main():
                    'horizon': args.horizon if args.mode == 'ppo' else None,
                    'updates_in_timed_region': state['updates'] if args.mode == 'ppo' else 0,
                    'parallelism': f'env-shard x{world}',
+                   'streams_per_gpu': args.shards,
                    'phys_general_envs_last_step': diag['phys_general_envs']},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                     'kernel': 'k_step (mas_step)', 'kernel_ms': kern_ms, 'bytes_per_env_step': b_env,
-                     'bytes_per_launch': b_env * n},
+                     'kernel': 'k_step (mas_step)' if args.shards == 1 else
+                     f'k_step (mas_step of one shard, {args.shards} shards on concurrent streams)',
+                     'kernel_ms': kern_ms, 'bytes_per_env_step': b_env,
+                     'bytes_per_launch': b_env * n_launch},
         'cpu_baseline': None,
     }
     # HBM traffic per mas_step from the committed rocprofv3 PMC passes of this
@@ -200,7 +226,7 @@ def main():
     if os.path.exists(tpath):
         tr_ = json.load(open(tpath))
         if tr_.get('workload') == f'{args.config}:{n}':
-            line['roofline']['traffic'] = tr_['traffic_bytes_per_step']
+            line['roofline']['traffic'] = tr_['traffic_bytes_per_step'] * n_launch / n
             line['roofline']['traffic_source'] = 'profiles/r01_pmc_traffic.json (FETCH_SIZE+WRITE_SIZE per mas_step)'
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(cfg)

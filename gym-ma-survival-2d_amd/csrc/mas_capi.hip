@@ -45,7 +45,8 @@ int64_t policy_blocks(int64_t M);
 hipError_t policy_pack(int D, const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                        const float* b3, void* packed, hipStream_t s);
 hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, void* xb, int64_t xb_stride,
-                      uint64_t seed, uint64_t step, int8_t* act, float* logp, float* value, hipStream_t s);
+                      uint64_t seed, uint64_t step, int64_t first_row, int8_t* act, float* logp, float* value,
+                      hipStream_t s);
 hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, int64_t xb_stride, const int8_t* act,
                         const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
                         float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
@@ -672,20 +673,28 @@ static bool policy_x_ok(int32_t obs_dim, int64_t x_stride)
     return x_stride >= ((obs_dim + 15) / 16) * 16 && x_stride % 8 == 0;
 }
 
-int mas_policy_act(const void* packed, int32_t obs_dim, int64_t n_rows, const float* obs, void* x_bf16,
-                   int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp, float* value,
-                   void* stream)
+int mas_policy_act_rows(const void* packed, int32_t obs_dim, int64_t n_rows, int64_t first_row, const float* obs,
+                        void* x_bf16, int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp,
+                        float* value, void* stream)
 {
-    if (!packed || obs_dim <= 0 || n_rows <= 0 || !obs || !actions || !logp || !value)
+    if (!packed || obs_dim <= 0 || n_rows <= 0 || first_row < 0 || !obs || !actions || !logp || !value)
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_act: bad argument");
     if (x_bf16 && !policy_x_ok(obs_dim, x_stride))
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_act: x_stride must be a multiple of 8 >= 16*ceil(obs_dim/16)");
     if ((reinterpret_cast<uintptr_t>(obs) & 15) || (reinterpret_cast<uintptr_t>(actions) & 1) ||
         (x_bf16 && (reinterpret_cast<uintptr_t>(x_bf16) & 15)))
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_act: misaligned buffer (obs/x 16 B, actions 2 B)");
-    HIP_TRY(policy_act(packed, obs_dim, n_rows, obs, x_bf16, x_stride, seed, step, actions, logp, value,
+    HIP_TRY(policy_act(packed, obs_dim, n_rows, obs, x_bf16, x_stride, seed, step, first_row, actions, logp, value,
                        (hipStream_t)stream));
     return MAS_OK;
+}
+
+int mas_policy_act(const void* packed, int32_t obs_dim, int64_t n_rows, const float* obs, void* x_bf16,
+                   int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp, float* value,
+                   void* stream)
+{
+    return mas_policy_act_rows(packed, obs_dim, n_rows, 0, obs, x_bf16, x_stride, seed, step, actions, logp, value,
+                               stream);
 }
 
 int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,

@@ -368,8 +368,9 @@ template <int KS>
 __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
                                                              int64_t M, const float* __restrict__ obs,
                                                              __bf16* __restrict__ xb, int64_t xb_stride,
-                                                             uint64_t seed, uint64_t step, int8_t* __restrict__ act,
-                                                             float* __restrict__ logp, float* __restrict__ value)
+                                                             uint64_t seed, uint64_t step, int64_t first_row,
+                                                             int8_t* __restrict__ act, float* __restrict__ logp,
+                                                             float* __restrict__ value)
 {
     __shared__ bf8 wl[kLdsFrag];
     const Layout Lo{ks1};
@@ -418,7 +419,9 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
     for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
     // Gumbel-max over each head; the RNG stream of k_sample (mas_capi.hip),
     // hardware exp2/log2 (the draws agree with k_sample up to ~1 ulp ties)
-    const uint64_t base = mix64(seed ^ mix64(step * 0x100000001B3ULL + (uint64_t)row));
+    // (keyed by the row's index in the whole batch: a shard launched with its
+    // first_row draws what the unsharded launch draws for those rows)
+    const uint64_t base = mix64(seed ^ mix64(step * 0x100000001B3ULL + (uint64_t)(first_row + row)));
     float lp = 0.0f;
     uint32_t packed_a[2] = {0u, 0u};
 #pragma unroll
@@ -743,12 +746,13 @@ hipError_t policy_pack(int D, const float* W1, const float* b1, const float* W2,
 int64_t policy_blocks(int64_t M) { return (M + 32 * pol::kWaves - 1) / (32 * pol::kWaves); }
 
 hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, void* xb, int64_t xb_stride,
-                      uint64_t seed, uint64_t step, int8_t* act, float* logp, float* value, hipStream_t s)
+                      uint64_t seed, uint64_t step, int64_t first_row, int8_t* act, float* logp, float* value,
+                      hipStream_t s)
 {
     const int ks1 = (D + 15) / 16;
     auto k = ks1 == 10 ? pol::k_policy_act<10> : ks1 == 9 ? pol::k_policy_act<9> : pol::k_policy_act<0>;
     hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
-                       ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, act, logp, value);
+                       ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, first_row, act, logp, value);
     return hipGetLastError();
 }
 

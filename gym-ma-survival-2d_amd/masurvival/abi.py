@@ -68,6 +68,8 @@ SIGNATURES = {
     'mas_policy_pack': (c_int32, [c_int32] + [c_void_p] * 8),
     'mas_policy_act': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_void_p, c_int64, ctypes.c_uint64,
                                  ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'mas_policy_act_rows': (c_int32, [c_void_p, c_int32, c_int64, c_int64, c_void_p, c_void_p, c_int64,
+                                      ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_policy_train': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                    c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
                          + [c_void_p] * 7),

@@ -245,18 +245,19 @@ class FusedPolicy:
         return x
 
     @torch.no_grad()
-    def act(self, obs, seed, step, actions, logp, value, xb=None):
+    def act(self, obs, seed, step, actions, logp, value, xb=None, first_row=0):
         """obs [M, D] fp32 rows -> actions int8 [M, 6], logp, value [M];
         xb [M, Dx] bf16 (optional, from x_buffer) receives the rows as the
-        update reads them."""
+        update reads them.  first_row: index of obs[0] in the whole batch when
+        the batch is launched in shards (the sampling RNG is keyed by it)."""
         M = obs.shape[0]
         assert obs.is_contiguous() and obs.dtype == torch.float32 and obs.shape[1] == self.D
         assert actions.is_contiguous() and logp.is_contiguous() and value.is_contiguous()
         xp = ctypes.c_void_p(xb.data_ptr()) if xb is not None else None
-        check(self.lib.mas_policy_act(ctypes.c_void_p(self.packed.data_ptr()), self.D, M, ctypes.c_void_p(obs.data_ptr()),
-                                      xp, self.Dx, int(seed), int(step), ctypes.c_void_p(actions.data_ptr()),
-                                      ctypes.c_void_p(logp.data_ptr()), ctypes.c_void_p(value.data_ptr()),
-                                      self._stream()))
+        check(self.lib.mas_policy_act_rows(ctypes.c_void_p(self.packed.data_ptr()), self.D, M, int(first_row),
+                                           ctypes.c_void_p(obs.data_ptr()), xp, self.Dx, int(seed), int(step),
+                                           ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(logp.data_ptr()),
+                                           ctypes.c_void_p(value.data_ptr()), self._stream()))
 
     def _buffers(self, M):
         if self._bufs is None or self._bufs['M'] != M:
@@ -405,6 +406,22 @@ class PPOTrainer:
     @torch.no_grad()
     def rollout_step(self, t):
         b = self.buf
+        if self.fused is not None and hasattr(self.env, 'shard_slices'):
+            # sharded env (vec_env.ShardedVecMaSurvival): each shard's policy
+            # forward + env step on its own stream, so one shard's act
+            # overlaps the others' env kernels; rows keep their global RNG key
+            A, D = b.A, b.D
+            self.env.fork()
+            for e, s, lo, hi in self.env.shard_slices():
+                with torch.cuda.stream(s):
+                    r0, r1 = lo * A, hi * A
+                    self.fused.act(b.obs[t].view(-1, D)[r0:r1], self.seed, self.steps_taken,
+                                   b.actions[t].view(-1, 6)[r0:r1], b.logp[t].view(-1)[r0:r1],
+                                   b.values[t].view(-1)[r0:r1], xb=b.xb[t][r0:r1], first_row=r0)
+                    e.step(b.actions[t][lo:hi], out=(b.obs[t + 1][lo:hi], b.rewards[t][lo:hi], b.dones[t][lo:hi]))
+            self.env.join()
+            self.steps_taken += 1
+            return
         if self.fused is not None:
             self.fused.act(b.obs[t].view(-1, b.D), self.seed, self.steps_taken, b.actions[t].view(-1, 6),
                            b.logp[t].view(-1), b.values[t].view(-1), xb=b.xb[t])

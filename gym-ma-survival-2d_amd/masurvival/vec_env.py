@@ -163,3 +163,99 @@ class VecMaSurvival:
 
 def torch_uint8():
     return _torch().uint8
+
+
+class ShardedVecMaSurvival:
+    """N envs as `shards` independent VecMaSurvival handles over consecutive
+    env ranges, each stepped on its own HIP stream.
+
+    The env step is latency-bound (one lane per env: at N = 65536 one wave per
+    SIMD, each kernel as long as its slowest wave), so independent shards on
+    separate streams overlap: one shard's kernels fill the SIMDs another
+    shard's tail leaves idle, and in the PPO rollout each shard's policy
+    forward overlaps the other shards' env kernels (`PPOTrainer` launches
+    act + step per shard through `shard_slices`).  Results are identical to
+    one handle over all N envs: env e keeps seed seeds[e], and the policy's
+    sampling RNG is keyed by the global row (`mas_policy_act_rows`).
+
+    `step` / `reset` order the shards after the caller's current stream and
+    the caller's stream after all shards, so callers see one env."""
+
+    def __init__(self, config: Optional[Dict[str, Dict[str, Any]]] = None, n_envs: int = 1, shards: int = 2,
+                 device=None, seeds: Optional[Sequence[int]] = None, auto_reset: bool = True):
+        torch = _torch()
+        n_envs, shards = int(n_envs), int(shards)
+        if shards < 1 or n_envs < shards:
+            raise ValueError('need 1 <= shards <= n_envs')
+        seeds = list(range(n_envs)) if seeds is None else list(seeds)
+        if len(seeds) != n_envs:
+            raise ValueError('need one seed per env')
+        bounds = [n_envs * k // shards for k in range(shards + 1)]
+        self.envs = [VecMaSurvival(config, n_envs=bounds[k + 1] - bounds[k], device=device,
+                                   seeds=seeds[bounds[k]:bounds[k + 1]], auto_reset=auto_reset)
+                     for k in range(shards)]
+        self.bounds = bounds
+        e0 = self.envs[0]
+        self.rc, self.device, self.auto_reset = e0.rc, e0.device, e0.auto_reset
+        self.n_envs, self.n_agents, self.obs_dim, self.layout = n_envs, e0.n_agents, e0.obs_dim, e0.layout
+        self.observation_space, self.action_space = e0.observation_space, e0.action_space
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(shards)]
+        N, A, D = n_envs, self.n_agents, self.obs_dim
+        self.obs = torch.zeros((N, A, D), dtype=torch.float32, device=self.device)
+        self.rewards = torch.zeros((N, A), dtype=torch.float32, device=self.device)
+        self.dones = torch.zeros((N,), dtype=torch.uint8, device=self.device)
+
+    def shard_slices(self):
+        """[(env, stream, first env, end env)] per shard."""
+        return [(e, s, self.bounds[k], self.bounds[k + 1]) for k, (e, s) in enumerate(zip(self.envs, self.streams))]
+
+    def fork(self):
+        """Shard streams wait for the caller's current stream."""
+        cur = _torch().cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(cur)
+
+    def join(self):
+        """The caller's current stream waits for every shard."""
+        cur = _torch().cuda.current_stream(self.device)
+        for s in self.streams:
+            cur.wait_stream(s)
+
+    def reset(self, mask=None):
+        torch = _torch()
+        self.fork()
+        for e, s, lo, hi in self.shard_slices():
+            with torch.cuda.stream(s):
+                o = e.reset(None if mask is None else mask[lo:hi])
+                self.obs[lo:hi].copy_(o)
+        self.join()
+        return self.obs
+
+    def step(self, actions, out=None):
+        torch = _torch()
+        obs, rew, done = (self.obs, self.rewards, self.dones) if out is None else out
+        self.fork()
+        for e, s, lo, hi in self.shard_slices():
+            with torch.cuda.stream(s):
+                e.step(actions[lo:hi], out=(obs[lo:hi], rew[lo:hi], done[lo:hi]))
+        self.join()
+        return obs, rew, done, {}
+
+    def flush_stats(self):
+        self.join()
+        return _torch().cat([e.flush_stats() for e in self.envs])
+
+    def debug_counters(self):
+        _torch().cuda.synchronize(self.device)
+        d = [e.debug_counters() for e in self.envs]
+        return {k: sum(x[k] for x in d) for k in d[0]}
+
+    def split(self, flat):
+        return self.envs[0].split(flat)
+
+    def state_bytes(self) -> int:
+        return sum(e.state_bytes() for e in self.envs)
+
+    def close(self):
+        for e in self.envs:
+            e.close()

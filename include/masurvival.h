@@ -179,6 +179,11 @@ int mas_sample_actions(int64_t n_rows, const float* logits, int64_t row_stride, 
  * mas_policy_train reads: columns [0, 16*ceil(obs_dim/16)) are written, the
  * row's obs_dim values, then 1.0 in column obs_dim (a bias column for the
  * caller's dW1 GEMM) when it falls in that range, then zeros.
+ * mas_policy_act_rows: the same for the rows [first_row, first_row + n_rows)
+ * of a larger batch (obs, x_bf16, actions, logp, value point at that slice):
+ * the sampling RNG is keyed by the row's index in the whole batch, so shards
+ * launched on separate streams draw exactly what one launch over the batch
+ * draws (mas_policy_act = first_row 0).
  *
  * mas_policy_train: forward of x_bf16 rows, the per-row gradient of the PPO
  * loss  mean(-min(r A, clip(r, 1-clip, 1+clip) A)) + vf_coef mean((v-ret)^2)
@@ -198,6 +203,9 @@ int mas_policy_pack(int32_t obs_dim, const float* w1, const float* b1, const flo
 int mas_policy_act(const void* packed, int32_t obs_dim, int64_t n_rows, const float* obs, void* x_bf16,
                    int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp, float* value,
                    void* stream);
+int mas_policy_act_rows(const void* packed, int32_t obs_dim, int64_t n_rows, int64_t first_row, const float* obs,
+                        void* x_bf16, int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp,
+                        float* value, void* stream);
 int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
                      const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
                      float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,

@@ -64,3 +64,26 @@ def test_hip_sampler_logp_and_distribution():
     acts3 = torch.empty_like(acts)
     sample_actions_hip(logits, 1234, 7, acts3, lp)
     assert torch.equal(acts, acts3)
+
+
+def test_sharded_rollout_matches_one_handle():
+    """ShardedVecMaSurvival (3 handles on 3 streams, per-shard act with the
+    global row key) fills the rollout buffer bit-identically to one handle."""
+    from masurvival.vec_env import ShardedVecMaSurvival
+    n, T = 4096, 6
+    tr = []
+    for env in (VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n)),
+                ShardedVecMaSurvival(C3_CONFIG, n_envs=n, shards=3, seeds=range(n))):
+        t_ = PPOTrainer(env, PPOConfig(horizon=8), seed=0)
+        for t in range(T):
+            t_.rollout_step(t)
+        tr.append(t_)
+    torch.cuda.synchronize()
+    b1, b2 = tr[0].buf, tr[1].buf
+    for name in ('obs', 'values'):
+        assert torch.equal(getattr(b1, name)[:T + 1], getattr(b2, name)[:T + 1]), name
+    for name in ('actions', 'logp', 'rewards', 'dones'):
+        assert torch.equal(getattr(b1, name)[:T], getattr(b2, name)[:T]), name
+    assert torch.equal(b1.xb[:T], b2.xb[:T])
+    for t_ in tr:
+        t_.env.close()
