@@ -4,6 +4,8 @@
 // allocation, and the small seed / stats kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -26,7 +28,8 @@ struct ClassInfo {
     ClassInfo class_info_##NAME();                                                                          \
     void launch_step_##NAME(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const int8_t*, float*, float*, \
                             uint8_t*, int);                                                                 \
-    void launch_reset_##NAME(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const uint8_t*, float*);
+    void launch_reset_##NAME(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const uint8_t*, float*); \
+    void launch_view_##NAME(hipStream_t, const Params&, const uint32_t*, int64_t, int64_t, float*);
 #ifdef MAS_HAVE_1v1
 MAS_DECLARE(1v1)
 #endif
@@ -285,6 +288,7 @@ struct Ops {
     ClassInfo info;
     void (*step)(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const int8_t*, float*, float*, uint8_t*, int);
     void (*reset)(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const uint8_t*, float*);
+    void (*view)(hipStream_t, const Params&, const uint32_t*, int64_t, int64_t, float*);
 };
 
 struct mas_handle {
@@ -478,16 +482,16 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     // capacity classes: (agents, heals, boxes, slots) -- see mas_k_<class>.hip
     bool ok = false;
 #ifdef MAS_HAVE_1v1
-    if (!ok && fits(2, 4, 4, 4)) { h->ops = Ops{class_info_1v1(), launch_step_1v1, launch_reset_1v1}; ok = true; }
+    if (!ok && fits(2, 4, 4, 4)) { h->ops = Ops{class_info_1v1(), launch_step_1v1, launch_reset_1v1, launch_view_1v1}; ok = true; }
 #endif
 #ifdef MAS_HAVE_2v2
-    if (!ok && fits(4, 4, 4, 4)) { h->ops = Ops{class_info_2v2(), launch_step_2v2, launch_reset_2v2}; ok = true; }
+    if (!ok && fits(4, 4, 4, 4)) { h->ops = Ops{class_info_2v2(), launch_step_2v2, launch_reset_2v2, launch_view_2v2}; ok = true; }
 #endif
 #ifdef MAS_HAVE_ffa
-    if (!ok && fits(4, 16, 16, 4)) { h->ops = Ops{class_info_ffa(), launch_step_ffa, launch_reset_ffa}; ok = true; }
+    if (!ok && fits(4, 16, 16, 4)) { h->ops = Ops{class_info_ffa(), launch_step_ffa, launch_reset_ffa, launch_view_ffa}; ok = true; }
 #endif
 #ifdef MAS_HAVE_xl
-    if (!ok && fits(8, 16, 16, 8)) { h->ops = Ops{class_info_xl(), launch_step_xl, launch_reset_xl}; ok = true; }
+    if (!ok && fits(8, 16, 16, 8)) { h->ops = Ops{class_info_xl(), launch_step_xl, launch_reset_xl, launch_view_xl}; ok = true; }
 #endif
     if (!ok) {
         delete h;
@@ -597,6 +601,36 @@ int mas_flush_stats(mas_handle* h, float* stats, void* stream)
     dim3 g((unsigned)((h->N + 255) / 256));
     hipLaunchKernelGGL(k_stats, g, dim3(256), 0, (hipStream_t)stream, h->state, h->N, h->ops.info.w_stats, stats);
     HIP_TRY(hipGetLastError());
+    return MAS_OK;
+}
+
+int mas_render_view(mas_handle* h, int64_t env, float* out)
+{
+    if (!h || !out || env < 0 || env >= h->N) return fail(MAS_ERR_INVALID_ARG, "mas_render_view: bad argument");
+    float* d = nullptr;
+    HIP_TRY(hipMalloc(&d, MAS_RENDER_VIEW_FLOATS * sizeof(float)));
+    HIP_TRY(hipMemset(d, 0, MAS_RENDER_VIEW_FLOATS * sizeof(float)));
+    HIP_TRY(hipDeviceSynchronize());
+    h->ops.view(nullptr, h->P, h->state, h->N, env, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, d, MAS_RENDER_VIEW_FLOATS * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    HIP_TRY(e);
+    // host-side header: floor size and the four walls (centre, angle, half extents)
+    out[10] = (float)h->P.floor_size;
+    float ex = 0.0f, ey = 0.0f;
+    for (int v = 0; v < 4; ++v) {
+        ex = std::max(ex, std::fabs(h->P.wall_poly.v[v].x));
+        ey = std::max(ey, std::fabs(h->P.wall_poly.v[v].y));
+    }
+    for (int k = 0; k < kNumWalls; ++k) {
+        float* w = out + 12 + 5 * k;
+        w[0] = h->P.wall_pos[k].x;
+        w[1] = h->P.wall_pos[k].y;
+        w[2] = h->P.wall_angle[k];
+        w[3] = ex;
+        w[4] = ey;
+    }
     return MAS_OK;
 }
 

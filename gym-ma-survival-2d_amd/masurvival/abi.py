@@ -63,6 +63,7 @@ SIGNATURES = {
     'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_sample_actions': (c_int32, [c_int64, c_void_p, c_int64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p,
                                      c_void_p]),
+    'mas_render_view': (c_int32, [c_void_p, c_int64, c_void_p]),
     'mas_policy_packed_bytes': (c_int64, [c_int32]),
     'mas_policy_blocks': (c_int64, [c_int64]),
     'mas_policy_pack': (c_int32, [c_int32] + [c_void_p] * 8),

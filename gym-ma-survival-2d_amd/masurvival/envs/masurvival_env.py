@@ -108,7 +108,13 @@ class MaSurvival:
         return stats
 
     def render(self, mode: str = 'human'):
-        raise NotImplementedError('rendering is out of scope for the MI355X build (not on the step path)')
+        """mode='rgb_array': a top-down uint8 [400, 400, 3] frame of the env
+        from device state (masurvival.render); 'human' needs pygame, which
+        this build does not have."""
+        if mode != 'rgb_array':
+            raise NotImplementedError("only render(mode='rgb_array') is available in the MI355X build")
+        from masurvival.render import render_env
+        return render_env(self._vec, 0)
 
     def close(self) -> None:
         self._vec.close()

@@ -27,6 +27,25 @@ def _torch():
     return torch
 
 
+MAS_RENDER_VIEW_FLOATS = 320  # include/masurvival.h
+
+
+def parse_render_view(v: np.ndarray) -> Dict[str, Any]:
+    """The float layout of mas_render_view (include/masurvival.h) as arrays."""
+    A, nb, ni, nh = (int(v[k]) for k in range(4))
+    AM, BM, HM = (int(v[k]) for k in range(7, 10))
+    o = 32
+    agents = v[o:o + 5 * AM].reshape(AM, 5)[:A]
+    o += 5 * AM
+    boxes = v[o:o + 5 * BM].reshape(BM, 5)[:nb]
+    o += 5 * BM
+    items = v[o:o + 4 * BM].reshape(BM, 4)[:ni]
+    o += 4 * BM
+    heals = v[o:o + 2 * HM].reshape(HM, 2)[:nh]
+    return {'agents': agents, 'boxes': boxes, 'items': items, 'heals': heals,
+            'zone': v[4:7].copy(), 'floor_size': float(v[10]), 'walls': v[12:32].reshape(4, 5).copy()}
+
+
 class VecMaSurvival:
     def __init__(self, config: Optional[Dict[str, Dict[str, Any]]] = None, n_envs: int = 1, device=None,
                  seeds: Optional[Sequence[int]] = None, auto_reset: bool = True):
@@ -135,6 +154,12 @@ class VecMaSurvival:
         out = (ctypes.c_int64 * 1)()
         check(self._lib.mas_debug_counters(self._h, out))
         return {'phys_general_envs': int(out[0])}
+
+    def render_view(self, env: int = 0) -> Dict[str, Any]:
+        """Bodies of env `env` for rendering (mas_render_view; synchronises)."""
+        buf = (ctypes.c_float * MAS_RENDER_VIEW_FLOATS)()
+        check(self._lib.mas_render_view(self._h, int(env), buf))
+        return parse_render_view(np.frombuffer(buf, dtype=np.float32).copy())
 
     def state_bytes(self) -> int:
         return int(self._lib.mas_state_bytes(self._h))

@@ -196,6 +196,20 @@ int mas_sample_actions(int64_t n_rows, const float* logits, int64_t row_stride, 
  * GEMMs), and
  * partials [mas_policy_blocks(n_rows)][4] = per-block sums of the clipped
  * surrogate loss, (v-ret)^2, entropy and the clipped-row count. */
+/* mas_render_view: one env's bodies for rendering (debugging / GIF frames;
+ * replaces what rendering.py:118-613 reads from the Box2D world).
+ * Synchronous: waits for the device, then copies MAS_RENDER_VIEW_FLOATS
+ * floats to host `out`:
+ *   [0] n_agents  [1] n_boxes  [2] n_box_items  [3] n_heals
+ *   [4..6] safe zone centre x, y, radius   [7..9] agent / box / heal slots
+ *   (AM, BM, HM of the capacity class)   [10] floor size
+ *   [12 + 5k] wall k = 0..3: centre x, y, angle, half extents x, y
+ *   [32 ...] AM agents (x, y, angle, alive, health), BM boxes (x, y, hx, hy,
+ *   health), BM box items (x, y, hx, hy), HM heals (x, y); entries past the
+ *   counts are unused. */
+#define MAS_RENDER_VIEW_FLOATS 320
+int mas_render_view(mas_handle* h, int64_t env, float* out);
+
 int64_t mas_policy_packed_bytes(int32_t obs_dim);
 int64_t mas_policy_blocks(int64_t n_rows);
 int mas_policy_pack(int32_t obs_dim, const float* w1, const float* b1, const float* w2, const float* b2,
