@@ -7,9 +7,10 @@ Added for the batched build: `--envs N` runs N envs of `VecMaSurvival` on the
 device (auto-reset, random actions drawn on the device) for --max-steps steps
 and reports agent-env-steps/s.
 
-Out of scope (they need pygame / a renderer, not on the step path): the
-interactive policy and --render / --screenshot / --gif, which exit with an
-error naming the missing feature.
+--screenshot / --gif record `render(mode='rgb_array')` frames (device state,
+masurvival.render) as in `demo.py:178-209`, written with PIL instead of
+imageio + gifsicle.  Out of scope (pygame): the interactive policy and
+--render (a window); they exit with an error naming the missing feature.
 
 usage: python -m masurvival.demo [random] [--max-steps N] [-c CONFIG.json]
                                  [--benchmark] [--envs N]"""
@@ -23,7 +24,7 @@ from typing import List, Optional
 import numpy as np
 
 ARGPARSE_DESC = ('Test the environment for one episode with a random policy '
-                 '(MI355X build; interactive play and rendering are not available).')
+                 '(MI355X build; interactive play and the pygame window are not available).')
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -37,10 +38,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument('-r', '--render', action='store_true', dest='render', default=False,
                     help='(not available in this build)')
     ap.add_argument('-s', '--screenshot', dest='screenshot_fpath', metavar='PATH', type=str, default=None,
-                    help='(not available in this build)')
+                    help='Record a frame of the episode to the given file (--screenshot-step picks it).')
     ap.add_argument('--screenshot-step', dest='screenshot_step', metavar='STEP', type=int, default=0)
     ap.add_argument('-g', '--gif', dest='gif_fpath', metavar='PATH', type=str, default=None,
-                    help='(not available in this build)')
+                    help='Record a GIF to the given file (one frame every --gif-record-interval steps).')
     ap.add_argument('--gif-record-interval', dest='gif_record_interval', metavar='N', type=int, default=10)
     ap.add_argument('--benchmark', dest='print_benchmark', action='store_true', default=False,
                     help='Print benchmark information at the end of the episode.')
@@ -62,24 +63,30 @@ def check_supported(args) -> None:
     missing = []
     if args.policy == 'interactive':
         missing.append('the interactive policy (pygame)')
-    if args.render or args.screenshot_fpath or args.gif_fpath:
-        missing.append('rendering (--render / --screenshot / --gif)')
+    if args.render:
+        missing.append('rendering to a window (--render)')
     if missing:
         raise SystemExit('not available in the MI355X build: ' + ', '.join(missing))
 
 
-def demo_env(env, max_steps: Optional[int] = None, print_benchmark: bool = False, seed: Optional[int] = None):
+def demo_env(env, max_steps: Optional[int] = None, print_benchmark: bool = False, seed: Optional[int] = None,
+             record=None):
     """One episode with a random policy (`demo.py:84-157`): until done or
-    max_steps; returns (stats, step times)."""
+    max_steps; `record(t, frame)` gets an rgb_array frame after the reset
+    and after each step; returns (stats, step times)."""
     times: List[float] = []
     t, obs, done = 0, env.reset(seed=seed), False
     env.action_space.seed(seed)
+    if record is not None:
+        record(t, env.render(mode='rgb_array'))
     while not done:
         action = env.action_space.sample()
         t0 = time.perf_counter()
         obs, reward, done, info = env.step(action)  # returns host arrays: synchronous
         times.append(time.perf_counter() - t0)
         t += 1
+        if record is not None:
+            record(t, env.render(mode='rgb_array'))
         if max_steps is not None and t == max_steps:
             print(f'Maximum number of steps {t} reached, terminating episode.')
             break
@@ -133,8 +140,28 @@ def main(argv=None) -> int:
         return 0
     from masurvival.envs.masurvival_env import MaSurvival
     env = MaSurvival(config=config)
-    demo_env(env, args.max_steps, args.print_benchmark, args.seed)
+    rec = {'screenshot': None, 'gif': []}
+
+    def record(t, frame):
+        if args.screenshot_fpath is not None and t == args.screenshot_step:
+            rec['screenshot'] = frame
+        if args.gif_fpath is not None and t % args.gif_record_interval == 0:
+            rec['gif'].append(frame)
+    want = args.screenshot_fpath is not None or args.gif_fpath is not None
+    demo_env(env, args.max_steps, args.print_benchmark, args.seed, record if want else None)
+    save_frames(args, rec)
     return 0
+
+
+def save_frames(args, rec) -> None:
+    """The recorded screenshot (PNG) and GIF (`demo.py:201-209`), via PIL."""
+    from PIL import Image
+    if args.screenshot_fpath is not None and rec['screenshot'] is not None:
+        print(f'Saving screenshot to {args.screenshot_fpath}.')
+        Image.fromarray(rec['screenshot']).save(args.screenshot_fpath)
+    if args.gif_fpath is not None and rec['gif']:
+        frames = [Image.fromarray(f) for f in rec['gif']]
+        frames[0].save(args.gif_fpath, save_all=True, append_images=frames[1:], duration=100, loop=0)
 
 
 if __name__ == '__main__':

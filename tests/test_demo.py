@@ -3,6 +3,8 @@ arguments): argument parsing, the JSON config loader and the unsupported
 options on CPU; one random-policy episode and the batched mode on the GPU."""
 import json
 
+import numpy as np
+
 import pytest
 
 from masurvival import demo
@@ -30,7 +32,7 @@ def test_json_config_loads_and_resolves(tmp_path):
     assert demo.load_config(None) is None
 
 
-@pytest.mark.parametrize('argv', [['interactive'], ['-r'], ['-s', 'a.png'], ['-g', 'a.gif']])
+@pytest.mark.parametrize('argv', [['interactive'], ['-r']])
 def test_unsupported_options_exit_with_a_message(argv):
     args = demo.build_parser().parse_args(argv)
     with pytest.raises(SystemExit, match='not available in the MI355X build'):
@@ -42,6 +44,20 @@ def test_demo_episode_and_benchmark_on_gpu(capsys):
     assert demo.main(['--max-steps', '30', '--benchmark', '--seed', '3']) == 0
     out = capsys.readouterr().out
     assert 'Episode complete' in out and 'Performance test results' in out and "'steps'" in out
+
+
+def test_frames_are_saved(tmp_path):
+    a = demo.build_parser().parse_args(['-s', str(tmp_path / 's.png'), '-g', str(tmp_path / 'e.gif')])
+    f = np.zeros((8, 8, 3), dtype=np.uint8)
+    demo.save_frames(a, {'screenshot': f, 'gif': [f, f + 50]})
+    assert (tmp_path / 's.png').stat().st_size > 0 and (tmp_path / 'e.gif').stat().st_size > 0
+
+
+@pytest.mark.gpu
+def test_demo_screenshot_and_gif_on_gpu(tmp_path):
+    assert demo.main(['--max-steps', '12', '-s', str(tmp_path / 's.png'), '--screenshot-step', '5',
+                      '-g', str(tmp_path / 'e.gif'), '--gif-record-interval', '4']) == 0
+    assert (tmp_path / 's.png').exists() and (tmp_path / 'e.gif').exists()
 
 
 @pytest.mark.gpu
