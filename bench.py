@@ -222,12 +222,13 @@ def main():
     }
     # HBM traffic per mas_step from the committed rocprofv3 PMC passes of this
     # workload (profiles/pmc_traffic.py); null when none matches
-    tpath = os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json')
+    tname = 'r01_pmc_traffic.json' if args.mode == 'env' else 'r01_pmc_traffic_ppo.json'
+    tpath = os.path.join(ROOT, 'profiles', tname)
     if os.path.exists(tpath):
         tr_ = json.load(open(tpath))
-        if tr_.get('workload') == f'{args.config}:{n}':
+        if tr_.get('workload') == f'{args.config}:{n}' + ('' if args.mode == 'env' else ':ppo'):
             line['roofline']['traffic'] = tr_['traffic_bytes_per_step'] * n_launch / n
-            line['roofline']['traffic_source'] = 'profiles/r01_pmc_traffic.json (FETCH_SIZE+WRITE_SIZE per mas_step)'
+            line['roofline']['traffic_source'] = f'profiles/{tname} (FETCH_SIZE+WRITE_SIZE per mas_step)'
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(cfg)
     if rank == 0:

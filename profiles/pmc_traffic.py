@@ -3,7 +3,8 @@ WRITE_SIZE collected in separate runs, MI355X_MICROARCH.md HBM section).
 
 usage: python profiles/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <out.json> <workload>
 
-Sums the env-step kernels (mas::k_*, excluding k_seed/k_stats) per step
+Sums the env-step kernels (mas::k_*, excluding k_seed/k_stats and the
+policy kernels mas::pol::*) per step
 (steps = number of k_pre dispatches).  FETCH_SIZE / WRITE_SIZE are in KB.
 The guide's x2 FETCH_SIZE correction is calibrated for 16-B-per-lane
 streaming reads; the state loads here are 4 B per lane (uncalibrated width),
@@ -18,7 +19,7 @@ def per_kernel(path, counter):
     acc = collections.defaultdict(float)
     n = collections.Counter()
     for r in csv.DictReader(open(path)):
-        if r['Counter_Name'] != counter or 'mas::' not in r['Kernel_Name']:
+        if r['Counter_Name'] != counter or 'mas::' not in r['Kernel_Name'] or '::pol::' in r['Kernel_Name']:
             continue
         k = r['Kernel_Name'].split('<')[0].replace('void mas::', '')
         acc[k] += float(r['Counter_Value']) * 1024.0

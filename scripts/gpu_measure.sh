@@ -15,6 +15,12 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mas::k_" --
 cd $R
 python profiles/pmc_traffic.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_write/run_counter_collection.csv $O/${TAG}_pmc_traffic.json 2v2:65536 > /dev/null || exit $?
 cp $O/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_traffic.json
+cd /tmp
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "mas::k_" --output-format csv -d $O/pmc_fetch_ppo -o run -- python3 $R/bench.py --no-cpu-baseline > $O/pmc_fetch_ppo.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mas::k_" --output-format csv -d $O/pmc_write_ppo -o run -- python3 $R/bench.py --no-cpu-baseline > $O/pmc_write_ppo.log 2>&1 || exit $?
+cd $R
+python profiles/pmc_traffic.py $O/pmc_fetch_ppo/run_counter_collection.csv $O/pmc_write_ppo/run_counter_collection.csv $O/${TAG}_pmc_traffic_ppo.json 2v2:65536:ppo > /dev/null || exit $?
+cp $O/${TAG}_pmc_traffic_ppo.json profiles/${TAG}_pmc_traffic_ppo.json
 timeout -k 10 400 python bench.py > $O/bench.log 2>&1 || exit $?
 timeout -k 10 200 python bench.py --mode env --no-cpu-baseline > $O/bench_env.log 2>&1 || exit $?
 timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_ffa.log 2>&1 || exit $?
