@@ -61,6 +61,25 @@ def main():
     for name, fn in rows:
         print(f'{name:28s} {bench(fn):.3f} ms', flush=True)
 
+    # the three GEMMs of one minibatch back to back vs on three streams
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    jobs = [lambda: nt(dz, h1), lambda: nt(da2, h1), lambda: nn(da1, xb[:, :D + 1])]
+
+    def serial():
+        for j in jobs:
+            j()
+
+    def concurrent():
+        cur = torch.cuda.current_stream()
+        for s_, j in zip(streams, jobs):
+            s_.wait_stream(cur)
+            with torch.cuda.stream(s_):
+                j()
+        for s_ in streams:
+            cur.wait_stream(s_)
+    print(f'{"g3+g2+g1 serial":28s} {bench(serial):.3f} ms', flush=True)
+    print(f'{"g3+g2+g1 on 3 streams":28s} {bench(concurrent):.3f} ms', flush=True)
+
 
 if __name__ == '__main__':
     main()
