@@ -1,21 +1,36 @@
 """Headline benchmark: agent-env-steps/sec for the 2v2 config.
 
 A "step" is one rollout step of every env on this rank, all in HBM: the
-shared policy MLP's forward on the current observations (bf16 autocast),
-Gumbel-max sampling of the six action heads, the batched MaSurvival.step (the
-HIP k_step kernel: actions -> 2 Box2D steps -> rules -> obs/rewards/done with
-auto-reset, writing straight into the rollout buffer), and -- every
---horizon steps -- the GAE scan (HIP mas_gae) plus one PPO update (1 epoch,
-4 minibatches, gradient all-reduce across ranks).  --mode env times the env
-kernel alone under a device-RNG random policy.
+fused policy kernel (MLP forward, bf16 MFMA with fp32 accumulation, plus
+Gumbel-max sampling of the six action heads: mas_policy_act), the batched
+MaSurvival.step (the HIP env kernels: actions -> 2 Box2D steps -> rules ->
+obs/rewards/done with auto-reset, written straight into the rollout buffer),
+and -- every --horizon steps -- the GAE scan (HIP mas_gae) plus one PPO update
+(1 epoch, 4 minibatches, gradient all-reduce across ranks).
+
+The timed window holds the work the metric names:
+  * an untimed pre-roll of --preroll full PPO iterations first puts the envs
+    and the policy in the training regime (general-path physics, contacts,
+    TOI), not the episode-start regime;
+  * after --warmup untimed steps, `align_steps` more untimed steps make the
+    K timed steps END on a horizon boundary, so the window contains
+    ceil(K / horizon) GAE + PPO updates (a short window is therefore
+    pessimistic: it carries a whole update for fewer rollout steps).
+--mode env times the env kernels alone under a device-RNG random policy.
 
 Run: python bench.py [--gpus N --steps K --warmup W --config 2v2 --envs N_per_gpu]
-For N>1 the driver launches one rank per GPU with torch.distributed.run; envs
-shard with no data-path collective (weak scaling).
+--gpus N > 1 without a torch.distributed launcher: bench.py starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child
+process (before touching the GPU), relays rank 0's JSON line and exits with
+the child's return code.  Envs shard with no data-path collective (weak
+scaling); n_gpus is the real world size.
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,10 +38,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'gym-ma-survival-2d_amd'))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+ENVS_DEFAULT = {'1v1': 4096, '2v2': 65536, 'ffa4': 16384}
 
 
 def algorithmic_bytes_per_env_step(A, H, B, D):
@@ -36,39 +50,91 @@ def algorithmic_bytes_per_env_step(A, H, B, D):
     return 8 * S + 6 * A + 4 * A * D + 4 * A + 1
 
 
-def cpu_baseline(cfg, budget_s=12.0):
-    """The C oracle (scalar restatement, 1 thread) on a bounded sample: round-robin
-    over 64 envs of the same config with uniform random actions, until budget_s."""
+def cpu_info():
+    model = '?'
+    try:
+        out = subprocess.run(['lscpu'], capture_output=True, text=True, timeout=10).stdout
+        model = next((ln.split(':', 1)[1].strip() for ln in out.splitlines() if ln.startswith('Model name')), '?')
+    except Exception:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:
+        avail = os.cpu_count() or 1
+    return model, avail
+
+
+def cpu_baseline(config, leg_s=6.0):
+    """The C oracle (scalar restatement, oracle/ora_bench.c: the whole loop in
+    C, no per-step ctypes call) on bounded samples, SURVEY.md 8(d):
+      (i)   1v1 (C1), 1 env, 1 thread;
+      (ii)  the bench config, 64 envs round-robin, 1 thread;
+      (iii) the bench config, T threads (T = min(16, CPUs this process may use:
+            the GPU box's per-GPU CPU share is 16)), 64 envs per thread.
+    Uniform-random actions, auto-reset.  `value` is leg (iii)."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
-    from oracle import OracleEnv
-    from masurvival.config import ResolvedConfig, pcg64_state
-    rc = ResolvedConfig(cfg)
-    n = 64
-    envs = [OracleEnv(rc.to_struct(), pcg64_state(s)) for s in range(n)]
-    for e in envs:
-        e.reset()
-    rng = np.random.default_rng(1)
-    acts = rng.integers(0, [3, 3, 3, 2, 2, 2], size=(256, n, rc.n_agents, 6)).astype(np.int8)
-    steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        a = acts[(steps // n) % 256]
-        for i, e in enumerate(envs):
-            _, _, d = e.step(a[i])
-            if d:
-                e.reset()
-        steps += n
-    dt = time.perf_counter() - t0
-    return {'value': steps * rc.n_agents / dt, 'unit': 'agent-env-steps/s', 'cores': 1, 'kind': 'port',
-            'sample': f'{steps} env-steps ({n} envs round-robin, random actions, auto-reset) of the C oracle, '
-                      f'1 thread, {dt:.1f}s incl. ctypes per-step call overhead'}
+    import oracle
+    from masurvival.config import NAMED_CONFIGS, ResolvedConfig, pcg64_state
+    model, avail = cpu_info()
+    threads = max(1, min(16, avail))
+    legs = []
+    for name, cfg_name, n, th in [('c1_1env_1thread', '1v1', 1, 1),
+                                  (f'{config}_64envs_1thread', config, 64, 1),
+                                  (f'{config}_{64 * threads}envs_{threads}threads', config, 64 * threads, threads)]:
+        rc = ResolvedConfig(NAMED_CONFIGS[cfg_name])
+        st = np.stack([pcg64_state(s) for s in range(n)])
+        steps, secs = oracle.bench_run(rc.to_struct(), st, th, leg_s)
+        legs.append({'leg': name, 'threads': th, 'env_steps': steps, 'seconds': round(secs, 3),
+                     'agent_env_steps_per_s': steps * rc.n_agents / secs})
+    out = {'value': legs[2]['agent_env_steps_per_s'], 'unit': 'agent-env-steps/s', 'cores': threads,
+           'kind': 'port',
+           'sample': f'C oracle (oracle/ora_bench.c), {config}, {64 * threads} envs on {threads} threads, '
+                     f'random actions + auto-reset, {legs[2]["seconds"]:.1f} s; other legs listed',
+           'cpu_model': model, 'cpus_available': avail, 'legs': legs}
+    proxy = os.path.join(ROOT, 'profiles', 'r02_reference_proxy.json')
+    if os.path.exists(proxy):
+        p = json.load(open(proxy))
+        out['reference_proxy'] = {
+            'what': 'reference Python env over the Box2D shim, 1 thread, timed in the build container '
+                    '(profiles/r02_reference_proxy.json; PyBox2D absent: a labelled proxy)',
+            'cpu_model': p.get('cpu_model'),
+            'agent_env_steps_per_s': {r['config']: r['agent_env_steps_per_s'] for r in p['results']}}
+    return out
 
 
-def main():
+def free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher: run torch.distributed.run as a child
+    process (nothing here has touched the GPU), relay its output, return its
+    exit code."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MAS_BENCH_CHILD='1')
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    for ln in p.stdout.splitlines():
+        if ln.startswith('{'):
+            print(ln, flush=True)
+        else:
+            print(ln, file=sys.stderr, flush=True)
+    return p.returncode
+
+
+def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=128, help='timed rollout steps (multiple of --horizon amortises the update)')
-    ap.add_argument('--warmup', type=int, default=64)
+    ap.add_argument('--steps', type=int, default=128, help='timed rollout steps')
+    ap.add_argument('--warmup', type=int, default=16)
+    ap.add_argument('--preroll', type=int, default=None,
+                    help='untimed PPO iterations (ppo mode, default 2) or env steps (env mode, default 128) '
+                         'before the warmup')
     ap.add_argument('--config', default='2v2')
     ap.add_argument('--envs', type=int, default=None, help='envs per GPU (default 65536 for 2v2)')
     ap.add_argument('--mode', choices=['ppo', 'env'], default='ppo',
@@ -78,11 +144,50 @@ def main():
     ap.add_argument('--lib', default=None, help='alternative libmas*.so (A/B variants)')
     ap.add_argument('--shards', type=int, default=1,
                     help='env handles per GPU, each on its own HIP stream (vec_env.ShardedVecMaSurvival)')
-    args = ap.parse_args()
+    return ap.parse_args()
 
+
+def dry_run(args, world, rank):
+    """MAS_BENCH_DRYRUN=1 (CPU tests of the launcher only): the rank set-up,
+    barrier + max-over-ranks timing and the JSON relay, with no env."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group('gloo')
+        dist.barrier()
+    t0 = time.perf_counter()
+    x = torch.zeros(1)
+    for _ in range(args.steps):
+        x += 1
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({'metric': 'dry-run', 'value': 0.0, 'n_gpus': world, 'steps': args.steps,
+                          'warmup': args.warmup, 'ms_per_step': dt * 1e3 / max(1, args.steps),
+                          'data': 'dry-run (launcher test, no env)'}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; n_gpus reports the world size',
+              file=sys.stderr)
+    if os.environ.get('MAS_BENCH_DRYRUN') == '1':
+        return dry_run(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
     # MAS_DIST_BACKEND=gloo and several ranks per GPU (local % devices) only
     # to rehearse the multi-rank path on a one-GPU box; the real run is RCCL
     backend = os.environ.get('MAS_DIST_BACKEND', 'nccl')
@@ -100,7 +205,7 @@ def main():
     from masurvival.config import NAMED_CONFIGS
     from masurvival.vec_env import VecMaSurvival
     cfg = NAMED_CONFIGS[args.config]
-    n = args.envs or {'1v1': 4096, '2v2': 65536, 'ffa4': 16384}[args.config]
+    n = args.envs or ENVS_DEFAULT[args.config]
     if args.shards > 1:
         from masurvival.vec_env import ShardedVecMaSurvival
         env = ShardedVecMaSurvival(cfg, n_envs=n, shards=args.shards, seeds=range(rank * n, rank * n + n),
@@ -109,45 +214,58 @@ def main():
         env = VecMaSurvival(cfg, n_envs=n, seeds=range(rank * n, rank * n + n), auto_reset=True)
     A, D = env.n_agents, env.obs_dim
     dev = env.device
-    # the env kernel's launch duration, HIP events on the stream it runs on
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    # the env kernels' launch-group duration, HIP events on the stream they run on
     kev = []
-    if args.shards > 1:
-        # one mas_step launch group per shard, timed on the shard's stream
-        for sub in env.envs:
-            def timed_shard_step(a, out=None, _step=sub.step):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                r = _step(a, out=out)
-                e1.record()
-                kev.append((e0, e1))
-                return r
-            sub.step = timed_shard_step
 
+    def timed(step_fn):
+        def f(a, out=None):
+            e0, e1 = ev(), ev()
+            e0.record()
+            r = step_fn(a, out=out)
+            e1.record()
+            kev.append((e0, e1))
+            return r
+        return f
+
+    if args.shards > 1:
+        for sub in env.envs:
+            sub.step = timed(sub.step)
+    else:
+        env.step = timed(env.step)
+
+    rev, uev = [], []  # whole rollout step / whole GAE + update, on the current stream
     if args.mode == 'ppo':
         from masurvival.ppo import PPOConfig, PPOTrainer
         pcfg = PPOConfig(horizon=args.horizon)
         tr = PPOTrainer(env, pcfg, seed=0)
-        env_step = env.step
-
-        def timed_env_step(a, out=None):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            r = env_step(a, out=out)
-            e1.record()
-            kev.append((e0, e1))
-            return r
-        if args.shards == 1:
-            env.step = timed_env_step
+        H = pcfg.horizon
         state = {'t': 0, 'updates': 0}
 
         def one_step():
+            e0, e1 = ev(), ev()
+            e0.record()
             tr.rollout_step(state['t'])
+            e1.record()
+            rev.append((e0, e1))
             state['t'] += 1
-            if state['t'] == pcfg.horizon:
+            if state['t'] == H:
+                u0, u1 = ev(), ev()
+                u0.record()
                 tr.finish_rollout()
                 tr.update()
+                u1.record()
+                uev.append((u0, u1))
                 state['t'] = 0
                 state['updates'] += 1
+        preroll = 2 if args.preroll is None else args.preroll
+        for _ in range(preroll * H):
+            one_step()
+        for _ in range(args.warmup):
+            one_step()
+        align = (-(state['t'] + args.steps)) % H
+        for _ in range(align):
+            one_step()
     else:
         env.reset()
         hi = torch.tensor([3, 3, 3, 2, 2, 2], device=dev, dtype=torch.int32)
@@ -158,19 +276,15 @@ def main():
         def one_step():
             u = torch.rand((n, A, 6), generator=gen, device=dev)
             acts.copy_((u * hi).to(torch.int8))
-            if args.shards > 1:
-                env.step(acts)
-                return
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
             env.step(acts)
-            e1.record()
-            kev.append((e0, e1))
-
-    for _ in range(args.warmup):
-        one_step()
+        preroll = 128 if args.preroll is None else args.preroll
+        align = 0
+        for _ in range(preroll + args.warmup):
+            one_step()
     torch.cuda.synchronize()
     kev.clear()
+    rev.clear()
+    uev.clear()
     if args.mode == 'ppo':
         state['updates'] = 0
     if world > 1:
@@ -184,20 +298,25 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
+    if args.mode == 'ppo' and state['updates'] != math.ceil(args.steps / H):
+        raise RuntimeError(f'timed window holds {state["updates"]} updates, expected {math.ceil(args.steps / H)}')
+    mean_ms = lambda evs: float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else 0.0  # noqa: E731
+    kern_ms, roll_ms, upd_ms = mean_ms(kev), mean_ms(rev), mean_ms(uev)
     if world > 1:
-        t = torch.tensor([dt, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, kern_ms, roll_ms, upd_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, kern_ms = float(t[0]), float(t[1])
+        dt, kern_ms, roll_ms, upd_ms = (float(x) for x in t)
 
     diag = env.debug_counters()
     total_agent_steps = world * n * A * args.steps
     b_env = algorithmic_bytes_per_env_step(A, env.rc.n_heals, env.rc.n_boxes, D)
     n_launch = n // args.shards  # envs per mas_step launch group (per shard when sharded)
     achieved = b_env * n_launch / (kern_ms * 1e-3) / 1e9
-    workload = (f'{args.config} PPO rollout (policy MLP 2x256 bf16 fwd + sample + env step + buffer), '
-                f'GAE + PPO update (1 epoch, 4 minibatches) every {args.horizon} steps'
-                if args.mode == 'ppo' else f'{args.config} env step, random policy')
+    if args.mode == 'ppo':
+        workload = (f'{args.config} PPO rollout (fused policy MLP 2x256 fwd + sample, env step into the rollout '
+                    f'buffer), GAE + PPO update (1 epoch, 4 minibatches) every {args.horizon} steps')
+    else:
+        workload = f'{args.config} env step, random policy'
     line = {
         'metric': 'agent-env-steps/sec (whole node), %s N_envs=%d' % (args.config, n * world),
         'value': total_agent_steps / dt,
@@ -205,32 +324,44 @@ def main():
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt * 1e3 / args.steps,
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'f32', 'data': 'synthetic (seeded envs, on-device policy sampling)',
+        'dtype': 'f32 env step; policy bf16 MFMA with f32 accumulate, f32 master weights + Adam'
+                 if args.mode == 'ppo' else 'f32',
+        'data': 'synthetic (seeded envs, on-device policy sampling)',
         'config': {'workload': workload, 'n_envs_per_gpu': n, 'n_agents': A, 'obs_dim': D,
                    'horizon': args.horizon if args.mode == 'ppo' else None,
+                   'preroll': (f'{preroll} PPO iterations ({preroll * args.horizon} steps + {preroll} updates)'
+                               if args.mode == 'ppo' else f'{preroll} env steps'),
+                   'align_steps': align,
                    'updates_in_timed_region': state['updates'] if args.mode == 'ppo' else 0,
                    'parallelism': f'env-shard x{world}',
                    'streams_per_gpu': args.shards,
-                   'phys_general_envs_last_step': diag['phys_general_envs']},
+                   'phys_general_envs_last_step': diag['phys_general_envs'],
+                   'breakdown_ms': {'env_step': kern_ms,
+                                    'rollout_step': roll_ms if args.mode == 'ppo' else None,
+                                    'gae_plus_update': upd_ms if args.mode == 'ppo' else None,
+                                    'amortised_step': (roll_ms + upd_ms / args.horizon)
+                                    if args.mode == 'ppo' else None}},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                     'kernel': 'k_step (mas_step)' if args.shards == 1 else
-                     f'k_step (mas_step of one shard, {args.shards} shards on concurrent streams)',
+                     'kernel': 'mas_step launch group (k_pre .. k_obs)' if args.shards == 1 else
+                     f'mas_step launch group of one shard ({args.shards} shards on concurrent streams)',
                      'kernel_ms': kern_ms, 'bytes_per_env_step': b_env,
                      'bytes_per_launch': b_env * n_launch},
         'cpu_baseline': None,
     }
     # HBM traffic per mas_step from the committed rocprofv3 PMC passes of this
-    # workload (profiles/pmc_traffic.py); null when none matches
-    tname = 'r01_pmc_traffic.json' if args.mode == 'env' else 'r01_pmc_traffic_ppo.json'
-    tpath = os.path.join(ROOT, 'profiles', tname)
-    if os.path.exists(tpath):
-        tr_ = json.load(open(tpath))
-        if tr_.get('workload') == f'{args.config}:{n}' + ('' if args.mode == 'env' else ':ppo'):
+    # same workload and regime (profiles/pmc_traffic.py); null when none matches
+    key = f'{args.config}:{n}:{args.mode}:preroll{preroll}'
+    for tname in sorted(os.listdir(os.path.join(ROOT, 'profiles')), reverse=True):
+        if not (tname.startswith('r0') and 'pmc_traffic' in tname and tname.endswith('.json')):
+            continue
+        tr_ = json.load(open(os.path.join(ROOT, 'profiles', tname)))
+        if tr_.get('workload') == key:
             line['roofline']['traffic'] = tr_['traffic_bytes_per_step'] * n_launch / n
             line['roofline']['traffic_source'] = f'profiles/{tname} (FETCH_SIZE+WRITE_SIZE per mas_step)'
+            break
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(cfg)
+        line['cpu_baseline'] = cpu_baseline(args.config)
     if rank == 0:
         print(json.dumps(line), flush=True)
     env.close()

@@ -299,7 +299,7 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
-    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path)
+    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count
     uint8_t* gen_flag;  // [N] env left the fast path this step
     float* sweep;
     mas_obs_layout layout;
@@ -505,8 +505,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
     h->P.prof = nullptr;
     h->phys = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 1) * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 1) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 2) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 2) * sizeof(int));
     h->sweep = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * 8 * sizeof(float));
     h->P.sweep = h->sweep;
@@ -516,6 +516,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.gen_flag = h->gen_flag;
     h->P.phys_list = h->phys;
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
+    h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
 #ifdef MAS_PROFILE
     if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(h->P.prof, 0, 64 * sizeof(unsigned long long));
@@ -674,6 +675,24 @@ int mas_debug_counters(mas_handle* h, int64_t* host_out)
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(&c, h->P.phys_count, sizeof(int), hipMemcpyDeviceToHost));
     host_out[0] = c;
+    return MAS_OK;
+}
+
+int mas_invalid_actions(mas_handle* h, int64_t* host_count, int32_t reset)
+{
+    if (!h || !host_count) return fail(MAS_ERR_INVALID_ARG, "mas_invalid_actions: null argument");
+    int c = 0;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&c, h->P.bad_actions, sizeof(int), hipMemcpyDeviceToHost));
+    if (reset) HIP_TRY(hipMemset(h->P.bad_actions, 0, sizeof(int)));
+    *host_count = c;
+    return MAS_OK;
+}
+
+int mas_debug_gen_flags(mas_handle* h, uint8_t* flags, void* stream)
+{
+    if (!h || !flags) return fail(MAS_ERR_INVALID_ARG, "mas_debug_gen_flags: null argument");
+    HIP_TRY(hipMemcpyAsync(flags, h->gen_flag, (size_t)h->N, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return MAS_OK;
 }
 

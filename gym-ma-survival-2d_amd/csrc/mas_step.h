@@ -887,14 +887,20 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
     for (int i = 0; i < C::AM; ++i)
 #pragma unroll
         for (int k = 0; k < 6; ++k) raw[i][k] = act[min(i, A - 1) * 6 + k];
+    // the reference asserts action_space.contains (masurvival_env.py:80);
+    // a kernel cannot raise: out-of-range entries are clamped and the env-step
+    // is counted in P.bad_actions (mas_invalid_actions reads it)
+    bool bad = false;
 #pragma unroll
     for (int i = 0; i < C::AM; ++i)
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             int x = i < A ? (int)raw[i][k] : 0;
             int hi = k < 3 ? 2 : 1;
+            bad = bad || x < 0 || x > hi;
             ac[i][k] = x < 0 ? 0 : (x > hi ? hi : x);
         }
+    if (bad) atomicAdd(P.bad_actions, 1);
     // ---------------- pre_step ----------------
     // boxes: Object.pre_step drops last step's queued box items (semantics.py:853-856)
 #pragma unroll

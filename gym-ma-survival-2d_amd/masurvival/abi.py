@@ -61,6 +61,8 @@ SIGNATURES = {
     'mas_gae': (c_int32, [c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
                           c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
+    'mas_invalid_actions': (c_int32, [c_void_p, POINTER(c_int64), c_int32]),
+    'mas_debug_gen_flags': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'mas_sample_actions': (c_int32, [c_int64, c_void_p, c_int64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p,
                                      c_void_p]),
     'mas_render_view': (c_int32, [c_void_p, c_int64, c_void_p]),

@@ -77,7 +77,10 @@ class MaSurvival:
 
     def _obs_dict(self, flat):
         host = flat[0].detach().cpu().numpy()
-        return {k: np.ascontiguousarray(v) for k, v in self._vec.split(host).items()}
+        x = {k: np.ascontiguousarray(v) for k, v in self._vec.split(host).items()}
+        # fetch_observations' own check (masurvival_env.py:656)
+        assert self.observation_space.contains(x), f'{x} not contained in the observation space {self.observation_space}'
+        return x
 
     def reset(self, seed: Optional[int] = None, return_info: bool = False, options: Optional[Dict] = None):
         if seed is not None:

@@ -117,16 +117,32 @@ class VecMaSurvival:
         check(self._lib.mas_reset(self._h, mptr, ctypes.c_void_p(self.obs.data_ptr()), self._stream()))
         return self.obs
 
-    def step(self, actions, out=None):
+    def step(self, actions, out=None, validate=False):
         """actions: int tensor [N,A,6] (MultiDiscrete [3,3,3,2,2,2]).
         out: optional (obs, rewards, done) tensors to write into (e.g. a
-        rollout-buffer slice); defaults to the env's own buffers."""
+        rollout-buffer slice); defaults to the env's own buffers.
+        validate: check every action against the action space first (the
+        reference's assert, masurvival_env.py:80; synchronises).  Without it
+        out-of-range entries are clamped on device and counted
+        (:meth:`invalid_actions`)."""
         torch = _torch()
         a = actions
+        N, A = self.n_envs, self.n_agents
+        if tuple(a.shape) != (N, A, 6):
+            raise ValueError(f'actions must have shape {(N, A, 6)}, got {tuple(a.shape)}')
+        if validate:
+            hi = torch.tensor([3, 3, 3, 2, 2, 2], device=a.device)
+            if bool(((a < 0) | (a >= hi)).any()):
+                raise AssertionError('Invalid action: outside MultiDiscrete([3, 3, 3, 2, 2, 2])')
         if a.dtype != torch.int8 or a.device != self.device or not a.is_contiguous():
             self._act.copy_(a)
             a = self._act
         obs, rew, done = (self.obs, self.rewards, self.dones) if out is None else out
+        if out is not None:
+            for t, shp, dt in ((obs, (N, A, self.obs_dim), torch.float32), (rew, (N, A), torch.float32),
+                               (done, (N,), torch.uint8)):
+                if tuple(t.shape) != shp or t.dtype != dt or not t.is_contiguous() or t.device != self.device:
+                    raise ValueError(f'out tensor must be contiguous {dt} {shp} on {self.device}')
         check(self._lib.mas_step(self._h, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(obs.data_ptr()),
                                  ctypes.c_void_p(rew.data_ptr()), ctypes.c_void_p(done.data_ptr()),
                                  int(self.auto_reset), self._stream()))
@@ -154,6 +170,22 @@ class VecMaSurvival:
         out = (ctypes.c_int64 * 1)()
         check(self._lib.mas_debug_counters(self._h, out))
         return {'phys_general_envs': int(out[0])}
+
+    def invalid_actions(self, reset: bool = True) -> int:
+        """Env-steps whose actions were out of range (clamped on device) since
+        the last reset of the count (mas_invalid_actions; synchronises)."""
+        out = ctypes.c_int64()
+        check(self._lib.mas_invalid_actions(self._h, ctypes.byref(out), int(reset)))
+        return int(out.value)
+
+    def gen_flags(self, out=None):
+        """uint8 [N] device tensor: 1 where the env left the contact-free
+        physics fast path in the last step (test diagnostics)."""
+        torch = _torch()
+        if out is None:
+            out = torch.empty((self.n_envs,), dtype=torch.uint8, device=self.device)
+        check(self._lib.mas_debug_gen_flags(self._h, ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
 
     def render_view(self, env: int = 0) -> Dict[str, Any]:
         """Bodies of env `env` for rendering (mas_render_view; synchronises)."""

@@ -230,6 +230,20 @@ int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const 
  * physics kernel (contacts, TOI events, box despawns). */
 int mas_debug_counters(mas_handle* h, int64_t* host_out);
 
+/* Action validation.  The reference asserts action_space.contains(actions)
+ * before every step (masurvival_env.py:80).  A kernel cannot raise, so
+ * mas_step clamps each out-of-range entry into MultiDiscrete([3,3,3,2,2,2])
+ * and counts the env-step; this returns that count since the handle was
+ * created or last reset (synchronises; reset != 0 zeroes it).  The Python
+ * facades check on the host before calling (MaSurvival.step always,
+ * VecMaSurvival.step(validate=True)). */
+int mas_invalid_actions(mas_handle* h, int64_t* host_count, int32_t reset);
+
+/* Test diagnostics: copies the per-env "left the contact-free fast path in
+ * the last mas_step" flags (uint8 [n_envs], device) into `flags`
+ * (stream-ordered; no synchronisation). */
+int mas_debug_gen_flags(mas_handle* h, uint8_t* flags, void* stream);
+
 const char* mas_last_error(void);
 int32_t mas_abi_version(void);
 

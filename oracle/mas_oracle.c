@@ -58,7 +58,7 @@ typedef ora_poly poly;
 /* coverage counters (tests assert the golden fixtures exercise each path) */
 enum { CNT_TOI_EVENT, CNT_TOI_RESTORE, CNT_SLEEP, CNT_BOX_BROKEN, CNT_BOX_PLACED, CNT_ITEM_PICKED,
        CNT_GIVE_OK, CNT_GIVE_LOST, CNT_DROP_ITEMS, CNT_HEAL_USED, CNT_DOUBLE_PICK, CNT_AA_CONTACT,
-       CNT_ISLAND_K, CNT_ISLANDS, CNT_ISLAND_K_GT2, CNT_ISLAND_K_GT4, CNT_ISLAND_K_GT8, CNT_N };
+       CNT_ISLAND_K, CNT_ISLANDS, CNT_ISLAND_K_GT2, CNT_ISLAND_K_GT4, CNT_ISLAND_K_GT8, CNT_TOI_CAP, CNT_N };
 static __thread int64_t g_cnt[CNT_N];
 void ora_counters(int64_t* out, int32_t reset)
 {
@@ -1146,7 +1146,7 @@ static void world_toi_agent(ora_world* w, step_scratch* sc, int i, float dt, int
         int minS = -1;
         for (int s = 0; s < ns; ++s) {
             if (!enabled[s]) continue;
-            if (count[s] > MAX_SUB_STEPS) continue;
+            if (count[s] > MAX_SUB_STEPS) { g_cnt[CNT_TOI_CAP]++; continue; } /* b2_maxSubSteps reached */
             float alpha;
             if (valid[s]) {
                 alpha = toi[s];

@@ -84,7 +84,7 @@ void ora_env_flush_stats(ora_env* e, float* stats /* MAS_STATS_WIDTH */);
 /* coverage counters: TOI events, TOI restores, sleeps, boxes broken/placed,
  * items picked, gives ok/lost, dropped items, heals used, double pickups,
  * agent-agent solver contacts */
-#define ORA_NCOUNTERS 12
+#define ORA_NCOUNTERS 18 /* ... plus island sizes and TOI sub-step cap hits (oracle.py COUNTER_NAMES) */
 void ora_counters(int64_t* out, int32_t reset);
 /* compact state digest for debugging (agent kinematics + health + inventory sizes) */
 int32_t ora_env_debug(const ora_env* e, float* out, int32_t cap);

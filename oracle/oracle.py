@@ -41,13 +41,16 @@ def lib():
         L.ora_env_debug.restype = c_int32
         L.ora_env_debug.argtypes = [c_void_p, POINTER(c_float), c_int32]
         L.ora_counters.argtypes = [POINTER(ctypes.c_int64), c_int32]
+        L.ora_bench_run.restype = c_int32
+        L.ora_bench_run.argtypes = [c_void_p, POINTER(c_uint64), ctypes.c_int64, c_int32, ctypes.c_double,
+                                    POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
 
 COUNTER_NAMES = ['toi_event', 'toi_restore', 'sleep', 'box_broken', 'box_placed', 'item_picked', 'give_ok',
                  'give_lost', 'drop_items', 'heal_used', 'double_pick', 'aa_contact', 'island_contacts', 'islands',
-                 'islands_k_gt2', 'islands_k_gt4', 'islands_k_gt8']
+                 'islands_k_gt2', 'islands_k_gt4', 'islands_k_gt8', 'toi_cap']
 
 
 def counters(reset=True):
@@ -109,3 +112,17 @@ class OracleEnv:
         out = np.zeros(512, dtype=np.float32)
         n = lib().ora_env_debug(self._h, _f32p(out), 512)
         return out[:n]
+
+
+def bench_run(cfg_struct, seed_states, threads=1, budget_s=5.0):
+    """CPU baseline loop (ora_bench.c): the envs with PCG64 states
+    seed_states [n, 6] stepped round-robin with uniform-random actions and
+    auto-reset on `threads` threads for about budget_s seconds, all in C.
+    Returns (env_steps, seconds)."""
+    st = np.ascontiguousarray(seed_states, dtype=np.uint64)
+    out = (ctypes.c_double * 2)()
+    rc = lib().ora_bench_run(ctypes.byref(cfg_struct), st.ctypes.data_as(POINTER(c_uint64)), st.shape[0],
+                             int(threads), float(budget_s), out)
+    if rc != 0:
+        raise RuntimeError('ora_bench_run failed')
+    return int(out[0]), float(out[1])

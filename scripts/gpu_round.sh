@@ -1,0 +1,42 @@
+#!/bin/bash
+# One GPU measurement pass (run via gpurun from the repo root):
+#   scripts/gpu_round.sh <tag> [tests] [smoke] [bench] [prof] [pmc] [env]
+# writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
+# script stops at the first failing step.
+R=$GRAFT_REPO_ROOT
+TAG=$1; shift
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+for step in "$@"; do
+  case $step in
+    tests)
+      cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { echo "tests failed"; exit 1; } ;;
+    regimes)
+      cd $R && MAS_DUMP_DIR=$O timeout -k 10 900 python -u -m pytest tests/test_gpu_parity_regimes.py -x -v -s \
+        --timeout 600 --timeout-method thread -p no:cacheprovider > $O/regimes.log 2>&1 || { echo "regimes failed"; exit 1; } ;;
+    smoke)
+      cd $R && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $? ;;
+    bench)
+      cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_driver.log 2>&1 || exit $?
+      cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $? ;;
+    env)
+      cd $R && timeout -k 10 200 python bench.py --mode env --no-cpu-baseline > $O/bench_env.log 2>&1 || exit $?
+      cd $R && timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_ffa.log 2>&1 || exit $?
+      cd $R && timeout -k 10 200 python bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline > $O/bench_1v1.log 2>&1 || exit $? ;;
+    prof)
+      cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- \
+        python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.log 2>&1 || exit $?
+      cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench128 -o run -- \
+        python3 $R/bench.py --no-cpu-baseline > $O/prof_bench128.log 2>&1 || exit $? ;;
+    pmc)
+      cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "mas::k_" --output-format csv \
+        -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || exit $?
+      cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mas::k_" --output-format csv \
+        -d $O/pmc_write -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_write.log 2>&1 || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  echo "step $step ok"
+done
+echo ok
