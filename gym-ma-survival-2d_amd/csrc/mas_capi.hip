@@ -491,7 +491,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (!ok && fits(4, 16, 16, 4)) { h->ops = Ops{class_info_ffa(), launch_step_ffa, launch_reset_ffa, launch_view_ffa}; ok = true; }
 #endif
 #ifdef MAS_HAVE_xl
-    if (!ok && fits(8, 16, 16, 8)) { h->ops = Ops{class_info_xl(), launch_step_xl, launch_reset_xl, launch_view_xl}; ok = true; }
+    if (!ok && fits(8, 8, 8, 4)) { h->ops = Ops{class_info_xl(), launch_step_xl, launch_reset_xl, launch_view_xl}; ok = true; }
 #endif
     if (!ok) {
         delete h;
@@ -517,6 +517,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.phys_list = h->phys;
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
     h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
+    h->P.toi_diag = nullptr;
 #ifdef MAS_PROFILE
     if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(h->P.prof, 0, 64 * sizeof(unsigned long long));
@@ -686,6 +687,13 @@ int mas_invalid_actions(mas_handle* h, int64_t* host_count, int32_t reset)
     HIP_TRY(hipMemcpy(&c, h->P.bad_actions, sizeof(int), hipMemcpyDeviceToHost));
     if (reset) HIP_TRY(hipMemset(h->P.bad_actions, 0, sizeof(int)));
     *host_count = c;
+    return MAS_OK;
+}
+
+int mas_debug_set_toi_counter(mas_handle* h, int32_t* counts)
+{
+    if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_debug_set_toi_counter: null handle");
+    h->P.toi_diag = counts;
     return MAS_OK;
 }
 

@@ -77,6 +77,7 @@ struct Params {
     int* phys_count;  // number of them
     uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)
     float* sweep;     // [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
+    int* toi_diag;    // test diagnostics (mas_debug_set_toi_counter): per env, TOI events + 65536 per capped SolveTOI
     int* bad_actions; // env-steps whose actions fell outside MultiDiscrete([3,3,3,2,2,2]) (clamped; mas_invalid_actions)
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };

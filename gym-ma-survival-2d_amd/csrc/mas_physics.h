@@ -1027,10 +1027,13 @@ MAS_HD bool toi_reject(const StaticG& g, V2 p0, V2 p1, float rB)
 
 // b2World::SolveTOI for agent I (events of different agents are independent:
 // statics never move and agent-agent pairs are not TOI pairs).
+// Returns the number of TOI events, + 65536 when a contact reached
+// b2_maxSubSteps (test diagnostics, Params::toi_diag).
 template <class C, class KT>
-__device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT& K, const StepScratch<C>& S, int I,
-                                          float dt)
+__device__ __forceinline__ int toi_agent(EnvL<C>& L, const Params& P, const KT& K, const StepScratch<C>& S, int I,
+                                         float dt)
 {
+    int events = 0;
     const float m = P.inv_mass, Ii = P.inv_I;
     Sweep sw;
     sw.c0 = sel(S.c0, I);
@@ -1132,6 +1135,7 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
             continue;
         }
         wake(L, I);
+        ++events;
         // island: the min contact first, then the agent's other touching statics
         uint32_t isl = 0;
         V2 iln[C::NS], ilp[C::NS];
@@ -1222,6 +1226,10 @@ __device__ __forceinline__ void toi_agent(EnvL<C>& L, const Params& P, const KT&
     for (int k = 0; k < 5; ++k) atomicMax(&P.prof[53 + k], tp[k]);
 #endif
 #undef MAS_LT
+    bool capped = false;
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) capped = capped || (s < ns && bit(enabled, s) && cnt[s] > 8);
+    return events + (capped ? 65536 : 0);
 }
 
 

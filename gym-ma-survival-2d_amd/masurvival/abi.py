@@ -14,6 +14,7 @@ from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_float, c_i
 MAS_MAX_ZONE_PHASES = 8
 MAS_MAX_KEYS = 16
 MAS_STATS_WIDTH = 19
+MAS_MAX_LASERS = 32
 
 
 class MasConfig(Structure):
@@ -34,6 +35,7 @@ class MasConfig(Structure):
         ('zone_damage', c_int32), ('zone_n_radii', c_int32), ('zone_radii', c_double * MAS_MAX_ZONE_PHASES),
         ('zone_random_centers', c_int32), ('zone_centers', (c_float * 2) * MAS_MAX_ZONE_PHASES),
         ('cam_depth', c_float), ('cam_fov', c_double), ('wall_aspect_ratio', c_double),
+        ('lidar_n_lasers', c_int32), ('lidar_depth', c_float), ('lidar_fov', c_double),
     ]
 
 
@@ -63,6 +65,7 @@ SIGNATURES = {
     'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_invalid_actions': (c_int32, [c_void_p, POINTER(c_int64), c_int32]),
     'mas_debug_gen_flags': (c_int32, [c_void_p, c_void_p, c_void_p]),
+    'mas_debug_set_toi_counter': (c_int32, [c_void_p, c_void_p]),
     'mas_sample_actions': (c_int32, [c_int64, c_void_p, c_int64, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p,
                                      c_void_p]),
     'mas_render_view': (c_int32, [c_void_p, c_int64, c_void_p]),

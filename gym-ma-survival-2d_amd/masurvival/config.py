@@ -19,7 +19,7 @@ from typing import Any, Dict, Optional
 
 import numpy as np
 
-from .abi import MasConfig, MAS_MAX_ZONE_PHASES
+from .abi import MAS_MAX_LASERS, MAS_MAX_ZONE_PHASES, MasConfig
 
 
 class CircleShape:
@@ -83,6 +83,12 @@ def merge_config(user_config: Optional[Dict[str, Dict[str, Any]]]) -> Dict[str, 
     config = copy.deepcopy(onevsone_heals_config)
     if user_config is not None:
         for k, sub in user_config.items():
+            if k == 'lidars':
+                # extension key: the reference defines Lidars
+                # (simulation.py:357-392) but never wires it into the env
+                # (masurvival_env.py:392, 857-858); here it is opt-in
+                config[k] = dict(sub)
+                continue
             config[k] |= sub  # KeyError on unknown k, as in the reference
     return config
 
@@ -124,6 +130,12 @@ class ResolvedConfig:
             raise IndexError('pop from empty list: more spawns than spawn-grid cells (semantics.py:77)')
         if c['gameover']['mode'] not in ('alldead', 'lastalive'):
             raise AssertionError('Invalid gameover mode')
+        self.lidars = c.get('lidars')
+        if self.lidars is not None:
+            n = int(self.lidars['n_lasers'])
+            if not 2 <= n <= MAS_MAX_LASERS:
+                # n_lasers = 1 divides by zero in Lidars._endpoints (simulation.py:388)
+                raise ValueError(f'lidars.n_lasers must be in [2, {MAS_MAX_LASERS}]')
 
     @property
     def agent_size(self) -> int:
@@ -194,6 +206,10 @@ class ResolvedConfig:
         s.cam_depth = float(c['cameras']['depth'])
         s.cam_fov = float(c['cameras']['fov'])
         s.wall_aspect_ratio = 100.0
+        if self.lidars is not None:
+            s.lidar_n_lasers = int(self.lidars['n_lasers'])
+            s.lidar_fov = float(self.lidars['fov'])
+            s.lidar_depth = float(self.lidars['depth'])
         return s
 
 

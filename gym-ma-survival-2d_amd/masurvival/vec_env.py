@@ -187,6 +187,17 @@ class VecMaSurvival:
         check(self._lib.mas_debug_gen_flags(self._h, ctypes.c_void_p(out.data_ptr()), self._stream()))
         return out
 
+    def set_toi_counter(self, counts=None):
+        """Test diagnostics: accumulate per-env SolveTOI events (+65536 per
+        agent that hit the sub-step cap) into the int32 [N] device tensor
+        `counts` on every step; None stops."""
+        if counts is not None:
+            torch = _torch()
+            assert counts.dtype == torch.int32 and counts.shape == (self.n_envs,) and counts.is_contiguous()
+        self._toi_counts = counts  # keep alive while the kernels write it
+        check(self._lib.mas_debug_set_toi_counter(self._h, None if counts is None else
+                                                   ctypes.c_void_p(counts.data_ptr())))
+
     def render_view(self, env: int = 0) -> Dict[str, Any]:
         """Bodies of env `env` for rendering (mas_render_view; synchronises)."""
         buf = (ctypes.c_float * MAS_RENDER_VIEW_FLOATS)()

@@ -75,7 +75,15 @@ typedef struct mas_config {
     float cam_depth;           /* cameras.depth                    (:173-176) */
     double cam_fov;            /* cameras.fov (radians, double as in Python) */
     double wall_aspect_ratio;  /* ThickRoomWalls default 100 (semantics.py:685) */
+    /* Lidars(n_lasers, fov, depth) (simulation.py:357-392) as the last agents
+     * module, observed as the 'lidars' key (the reference leaves
+     * the module unwired, masurvival_env.py:392,857-858).  0 = off. */
+    int32_t lidar_n_lasers;    /* lidars.n_lasers (0, or 2..MAS_MAX_LASERS) */
+    float lidar_depth;         /* lidars.depth */
+    double lidar_fov;          /* lidars.fov (radians, double as in Python) */
 } mas_config;
+
+#define MAS_MAX_LASERS 32
 
 /* Observation layout: one flat float32 row of `obs_dim` per agent; the keys
  * are laid out in observation_space (gym Dict, sorted-key) order, each key's
@@ -243,6 +251,12 @@ int mas_invalid_actions(mas_handle* h, int64_t* host_count, int32_t reset);
  * the last mas_step" flags (uint8 [n_envs], device) into `flags`
  * (stream-ordered; no synchronisation). */
 int mas_debug_gen_flags(mas_handle* h, uint8_t* flags, void* stream);
+
+/* Test diagnostics: while `counts` (device int32 [n_envs], or NULL to stop)
+ * is set, every mas_step adds per env the number of b2World::SolveTOI
+ * events of its agents, plus 65536 for each agent whose SolveTOI reached
+ * Box2D's sub-step cap (b2_maxSubSteps = 8 per contact). */
+int mas_debug_set_toi_counter(mas_handle* h, int32_t* counts);
 
 const char* mas_last_error(void);
 int32_t mas_abi_version(void);

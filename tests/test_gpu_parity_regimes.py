@@ -76,18 +76,22 @@ def test_shard_size_sampled_envs_match_oracle(name, cfg, n, T):
 
 
 def test_ppo_regime_policy_actions_match_oracle():
-    """Policy-driven parity at the headline size: 3 fused-PPO iterations
-    (2v2 x65536, horizon 64) record every action; the 256 envs with the most
-    general-path steps plus random envs are replayed through the oracle with
-    those actions (auto-reset), bit-exact obs / reward / done, and the
-    replay must exercise TOI events and hit Box2D's sub-step cap."""
+    """Policy-driven parity at the headline size: 4 fused-PPO iterations
+    (2v2 x65536, horizon 64) record every action and, per env, the GPU's
+    general-path steps and SolveTOI events / sub-step-cap hits.  The envs
+    that hit the cap, those with the most TOI events and the most
+    general-path steps, plus fixed and random envs, are replayed through the
+    oracle with those actions (auto-reset): bit-exact obs / reward / done,
+    and the oracle must hit the cap on exactly the same envs."""
     from masurvival.ppo import PPOConfig, PPOTrainer
     rc = ResolvedConfig(C3_CONFIG)
-    n, H, iters = 65536, 64, 3
+    n, H, iters = 65536, 64, 4
     env = make_vec(C3_CONFIG, n, range(n))
     tr = PPOTrainer(env, PPOConfig(horizon=H), seed=0)
     assert tr.fused is not None
     gen_cnt = torch.zeros((n,), dtype=torch.int32, device=env.device)
+    toi_cnt = torch.zeros((n,), dtype=torch.int32, device=env.device)
+    env.set_toi_counter(toi_cnt)
     flags = torch.empty((n,), dtype=torch.uint8, device=env.device)
     acts, rews, dones = [], [], []
     for _ in range(iters):
@@ -104,11 +108,18 @@ def test_ppo_regime_policy_actions_match_oracle():
     dones = np.concatenate(dones)  # [iters*H, N]
     assert env.invalid_actions() == 0
     gen = gen_cnt.cpu().numpy()
+    toi = toi_cnt.cpu().numpy()
+    env.set_toi_counter(None)
     env.close()
     del tr
-
-    top = np.argsort(-gen, kind='stable')[:256]
-    cands = sorted(set(top.tolist()) | set(_sample(n, 8, 3)))
+    caps, events = toi >> 16, toi & 0xffff
+    assert caps.sum() > 0, 'no SolveTOI reached the sub-step cap in the PPO regime'
+    # replay: the envs whose SolveTOI hit the cap, then the most TOI events,
+    # then the most general-path steps, plus fixed / random envs
+    pick = set(np.argsort(-caps, kind='stable')[:min(64, int((caps > 0).sum()))].tolist())
+    pick |= set(np.argsort(-events, kind='stable')[:64].tolist())
+    pick |= set(np.argsort(-gen, kind='stable')[:128].tolist())
+    cands = sorted(pick | set(_sample(n, 8, 3)))
     # second pass: the same actions through a fresh handle, gathering the
     # candidates' observations (the env is deterministic given seeds + actions)
     env2 = make_vec(C3_CONFIG, n, range(n))
@@ -135,8 +146,12 @@ def test_ppo_regime_policy_actions_match_oracle():
         per_env[e] = oracle.counters(True)
     tot = {k: sum(c[k] for c in per_env.values()) for k in oracle.COUNTER_NAMES}
     capped = sorted(((c['toi_cap'], c['toi_event'], e) for e, c in per_env.items()), reverse=True)
-    print('ppo-regime replay: general-path steps (max / median of replayed) %d / %d; counters %s; '
-          'most capped env %s' % (gen.max(), int(np.median(gen[cands])), json.dumps(tot), capped[:3]))
+    print('ppo-regime replay: %d envs; general-path steps max %d; GPU SolveTOI events max %d, capped envs %d; '
+          'oracle counters over the replay %s; most capped env %s' % (
+              len(cands), gen.max(), events.max(), int((caps > 0).sum()), json.dumps(tot), capped[:3]))
+    # the oracle sees the same cap hits as the GPU on every replayed env
+    for e in cands:
+        assert (per_env[e]['toi_cap'] > 0) == (caps[e] > 0), (e, per_env[e], toi[e])
     dump = os.environ.get('MAS_DUMP_DIR')
     if dump:
         os.makedirs(dump, exist_ok=True)
