@@ -1234,6 +1234,303 @@ __device__ __forceinline__ int toi_agent(EnvL<C>& L, const Params& P, const KT& 
 
 
 // ---------------------------------------------------------------------------
+// Lane-group b2World::SolveTOI (k_gen_toi): G lanes per (env, agent) and
+// lane s of the group owns static s (walls 0..3, then the boxes).  What is
+// independent per static runs on its own lane -- the conservative pre-test
+// and b2TimeOfImpact against the agent's sweep, the narrowphase update of
+// each contact (b2Contact::Update) when the island is built -- and the
+// minimum TOI is a butterfly reduction over the group (ties: lowest static,
+// as the serial scan's strict <).  The TOI island solve (position then
+// velocity iterations) is Gauss-Seidel over the island's contacts in
+// Box2D's order (the min contact, then the agent's other touching contacts);
+// every lane of the group runs it on the same values, so the group stays
+// uniform.  Each contact's constraint data (normal, plane point; the
+// velocity constraint) is computed once per event instead of once per
+// iteration -- the same operations on the same inputs, so the same bits.
+// Same results as toi_agent / world_toi_agent (oracle/mas_oracle.c).
+// ---------------------------------------------------------------------------
+template <class C>
+constexpr int kToiG = C::NS <= 8 ? 8 : (C::NS <= 16 ? 16 : 32);
+
+// value of lane `src` (group-relative) of this lane's group
+template <int G, class T>
+__device__ __forceinline__ T gshfl(T v, int src)
+{
+    const int base = (int)(threadIdx.x & 63) & ~(G - 1);
+    return __shfl(v, base + src, 64);
+}
+
+// pc_solve_as / vc_init_as with the contact's normal and plane point given
+// (rmul(sq, ln), xmul(sp, sq, lp) hoisted by the caller): identical ops
+MAS_HD float pc_solve_as_h(V2 normal, V2 planePoint, V2 sp, V2& cB, float& aB, float r, float m, float I,
+                           float baum)
+{
+    V2 clip = cB;
+    float sep = dot(sub(clip, planePoint), normal) - kPolyRadius - r;
+    V2 point = clip;
+    V2 rA = sub(point, sp), rB = sub(point, cB);
+    float Cc = clamp_b2(baum * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+    const float mA = 0.0f, iA = 0.0f;
+    float rnA = cross(rA, normal), rnB = cross(rB, normal);
+    float K = mA + m + iA * rnA * rnA + I * rnB * rnB;
+    float imp = K > 0.0f ? -Cc / K : 0.0f;
+    V2 Pp = scl(imp, normal);
+    cB = add(cB, scl(m, Pp));
+    aB += I * cross(rB, Pp);
+    return sep;
+}
+
+MAS_HD VC vc_init_as_h(V2 normal, V2 planePoint, V2 sp, V2 cB, float rB, float mB, float iB)
+{
+    VC k;
+    V2 clip = cB;
+    V2 wcA = add(clip, scl(kPolyRadius - dot(sub(clip, planePoint), normal), normal));
+    V2 wcB = sub(clip, scl(rB, normal));
+    V2 point = scl(0.5f, add(wcA, wcB));
+    k.normal = normal;
+    k.rA = sub(point, sp);
+    k.rB = sub(point, cB);
+    const float mA = 0.0f, iA = 0.0f;
+    float rnA = cross(k.rA, normal), rnB = cross(k.rB, normal);
+    float kn = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+    k.nm = kn > 0.0f ? 1.0f / kn : 0.0f;
+    V2 t = cross_vs(normal, 1.0f);
+    float rtA = cross(k.rA, t), rtB = cross(k.rB, t);
+    float kt = mA + mB + iA * rtA * rtA + iB * rtB * rtB;
+    k.tm = kt > 0.0f ? 1.0f / kt : 0.0f;
+    k.ni = 0.0f;
+    k.ti = 0.0f;
+    return k;
+}
+
+// the position of static q (compile-time q): walls from P, boxes from L
+template <class C>
+MAS_HD V2 static_pos(const EnvL<C>& L, const Params& P, int q)
+{
+    return q < kNumWalls ? P.wall_pos[q] : L.bp[q - kNumWalls];
+}
+
+struct ToiGroupOut {
+    V2 c, v;
+    float a, w;
+    uint32_t touch;  // touching bits of the group's statics (s < ns), final
+    int events;      // TOI events, + 65536 if a contact reached b2_maxSubSteps
+};
+
+// SolveTOI of agent I (awake, alive) for lane s of its group.  c0/a0: the
+// agent's sweep start (b2Sweep c0/a0 of this world step); L: the env after
+// the island solve; K: the contact memory in HBM (impulse resets of this
+// lane's contact are written there); t0: agent I's touching word.
+template <class C, int G>
+__device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const Params& P,
+                                                       const Cont<C, ContGlbStore<C>>& K, int I, int s, V2 c0,
+                                                       float a0, uint32_t t0, float dt)
+{
+    static_assert(G >= C::NS && G <= 64 && (G & (G - 1)) == 0, "one lane per static");
+    const float r = P.agent_r, m = P.inv_mass, Ii = P.inv_I;
+    const int ns = kNumWalls + L.nbox;
+    const bool mine = s < ns;
+    const StaticG g = static_geom_dyn(L, P, s < C::NS ? s : C::NS - 1);
+    const ToiPoly T = toi_poly(g.poly, g.p, g.angle);
+    Sweep sw;
+    sw.c0 = c0;
+    sw.a0 = a0;
+    sw.c = sel(L.c, I);
+    sw.a = sel(L.a, I);
+    sw.alpha0 = 0.0f;
+    V2 vB = sel(L.v, I);
+    float wB = sel(L.w, I);
+    bool touch = mine && ((t0 >> s) & 1u);
+    bool en = true, val = false;
+    int cnt = 0;
+    float toi = 1.0f;
+    int events = 0;
+    const int lane = (int)(threadIdx.x & 63);
+    const int base = lane & ~(G - 1);
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << base;
+#ifdef MAS_PROFILE
+    // per group: TOI calls, position iterations, phase times (constant clock)
+    unsigned long long ntoi = 0, npos = 0, lt = wall_clock64(), tp[5] = {0, 0, 0, 0, 0};
+#define MAS_GT(k)                                     \
+    do {                                              \
+        const unsigned long long n_ = wall_clock64(); \
+        tp[k] += n_ - lt;                             \
+        lt = n_;                                      \
+    } while (0)
+#else
+#define MAS_GT(k) ((void)0)
+#endif
+    for (int guard = 0; guard < 9 * C::NS + 1; ++guard) {
+        // (1) this lane's stale TOI: conservative pre-test, else b2TimeOfImpact
+        if (mine && en && cnt <= 8 && !val) {
+            float alpha = 1.0f;
+            if (!toi_reject(g, sw.c0, sw.c, r)) {
+                float beta;
+#ifdef MAS_PROFILE
+                ++ntoi;
+#endif
+                const int st = time_of_impact(T, sw, r, beta);
+                if (st == kToiTouching) alpha = fmin_b2(sw.alpha0 + (1.0f - sw.alpha0) * beta, 1.0f);
+            }
+            toi = alpha;
+            val = true;
+        }
+        MAS_GT(0);
+        // (2) group minimum over the candidates with alpha < 1
+        float ma = (mine && en && cnt <= 8 && toi < 1.0f) ? toi : 2.0f;
+        int ms = s;
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+            const float oa = __shfl_xor(ma, o, 64);
+            const int os = __shfl_xor(ms, o, 64);
+            if (oa < ma || (oa == ma && os < ms)) {
+                ma = oa;
+                ms = os;
+            }
+        }
+        if (ma >= 1.0f || 1.0f - 10.0f * kEps < ma) break;
+        const int minS = ms;
+        const float minAlpha = ma;
+        const Sweep backup = sw;
+        {
+            const float beta = (minAlpha - sw.alpha0) / (1.0f - sw.alpha0);
+            sw.c0 = add(sw.c0, scl(beta, sub(sw.c, sw.c0)));
+            sw.a0 += beta * (sw.a - sw.a0);
+            sw.alpha0 = minAlpha;
+            sw.c = sw.c0;
+            sw.a = sw.a0;
+        }
+        // (3) b2Contact::Update of the min contact on its lane
+        V2 ln = mk(0.0f, 0.0f), lp = mk(0.0f, 0.0f);
+        int tch = 0;
+        if (s == minS) {
+            const bool t = collide_pc(g.poly, g.p, g.q, sw.c, kPolyRadius, r, ln, lp);
+            if (!(t && touch)) {
+                K.set_asni(I, s, 0.0f);
+                K.set_asti(I, s, 0.0f);
+            }
+            touch = t;
+            tch = t ? 1 : 0;
+            val = false;
+            ++cnt;
+        }
+        if (!gshfl<G>(tch, minS)) {
+            if (s == minS) en = false;
+            sw = backup;
+            continue;
+        }
+        ++events;
+        // (4) the island: every other contact of the agent is updated (and re-enabled)
+        if (mine && s != minS) {
+            en = true;
+            const bool t = collide_pc(g.poly, g.p, g.q, sw.c, kPolyRadius, r, ln, lp);
+            if (!(t && touch)) {
+                K.set_asni(I, s, 0.0f);
+                K.set_asti(I, s, 0.0f);
+            }
+            touch = t;
+        }
+        const uint32_t isl = (uint32_t)((__ballot(mine && touch) & gmask) >> base);
+        // (5) constraint data of every island contact, once per event
+        const V2 nrm = rmul(g.q, ln), ppt = xmul(g.p, g.q, lp);
+        const V2 nm = mk(gshfl<G>(nrm.x, minS), gshfl<G>(nrm.y, minS));
+        const V2 pm = mk(gshfl<G>(ppt.x, minS), gshfl<G>(ppt.y, minS));
+        const V2 sm = mk(gshfl<G>(g.p.x, minS), gshfl<G>(g.p.y, minS));
+        V2 nq[C::NS], pq[C::NS];
+#pragma unroll
+        for (int q = 0; q < C::NS; ++q) {
+            nq[q] = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
+            pq[q] = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
+        }
+        MAS_GT(1);
+        // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
+        V2 cB = sw.c;
+        float aB = sw.a;
+        for (int it = 0; it < 20; ++it) {
+#ifdef MAS_PROFILE
+            ++npos;
+#endif
+            float minsep = 0.0f;
+            minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, sm, cB, aB, r, m, Ii, kToiBaumgarte));
+#pragma unroll
+            for (int q = 0; q < C::NS; ++q) {
+                if (!bit(isl, q) || q == minS) continue;
+                minsep = fmin_b2(minsep, pc_solve_as_h(nq[q], pq[q], static_pos(L, P, q), cB, aB, r, m, Ii,
+                                                       kToiBaumgarte));
+            }
+            if (minsep >= -1.5f * kLinearSlop) break;
+        }
+        MAS_GT(2);
+        sw.c0 = cB;
+        sw.a0 = aB;
+        // ... then 10 velocity iterations without warm starting
+        VC km = vc_init_as_h(nm, pm, sm, cB, r, m, Ii);
+        constexpr bool kHoist = C::NS <= 8;  // register budget: hoist every contact's constraint only for small classes
+        VC kq[kHoist ? C::NS : 1];
+        float ni[C::NS], ti[C::NS];
+#pragma unroll
+        for (int q = 0; q < C::NS; ++q) {
+            ni[q] = 0.0f;
+            ti[q] = 0.0f;
+            if (kHoist) kq[kHoist ? q : 0] = vc_init_as_h(nq[q], pq[q], static_pos(L, P, q), cB, r, m, Ii);
+        }
+        for (int it = 0; it < 10; ++it) {
+            {
+                V2 vz = mk(0.0f, 0.0f);
+                float wz = 0.0f;
+                vc_solve(km, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+            }
+#pragma unroll
+            for (int q = 0; q < C::NS; ++q) {
+                if (!bit(isl, q) || q == minS) continue;
+                VC k = kHoist ? kq[kHoist ? q : 0] : vc_init_as_h(nq[q], pq[q], static_pos(L, P, q), cB, r, m, Ii);
+                k.ni = ni[q];
+                k.ti = ti[q];
+                V2 vz = mk(0.0f, 0.0f);
+                float wz = 0.0f;
+                vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                ni[q] = k.ni;
+                ti[q] = k.ti;
+            }
+        }
+        MAS_GT(3);
+        const float h = (1.0f - minAlpha) * dt;
+        integrate(cB, aB, vB, wB, h);
+        sw.c = cB;
+        sw.a = aB;
+        val = false;
+        MAS_GT(4);
+    }
+    ToiGroupOut o;
+    o.c = sw.c;
+    o.a = sw.a;
+    o.v = vB;
+    o.w = wB;
+    o.touch = (uint32_t)((__ballot(mine && touch) & gmask) >> base);
+    const bool capped = (__ballot(mine && en && cnt > 8) & gmask) != 0ull;
+    o.events = events + (capped ? 65536 : 0);
+#ifdef MAS_PROFILE
+    // same slots as toi_agent's profile (profiles/prof_toi.py): max per group
+    // of events / TOI calls (summed over the group's lanes) / position
+    // iterations, totals, and the longest time per phase (0 TOI, 1 min +
+    // narrowphase + island gather, 2 position, 3 velocity, 4 integrate)
+    unsigned long long gt = ntoi;
+#pragma unroll
+    for (int o2 = 1; o2 < G; o2 <<= 1) gt += __shfl_xor(gt, o2, 64);
+    if (s == 0) {
+        atomicMax(&P.prof[48], (unsigned long long)events);
+        atomicMax(&P.prof[49], gt);
+        atomicMax(&P.prof[50], npos);
+        atomicAdd(&P.prof[51], (unsigned long long)events);
+        atomicAdd(&P.prof[52], gt);
+        for (int k = 0; k < 5; ++k) atomicMax(&P.prof[53 + k], tp[k]);
+    }
+#endif
+#undef MAS_GT
+    return o;
+}
+
+// ---------------------------------------------------------------------------
 // Contact-free fast path of one world.Step (speculative).  Valid while the
 // env has no contact memory, no pair reaches touching distance and no TOI
 // sweep can hit a static: then Box2D's step is damping + integrate + sleep

@@ -53,8 +53,8 @@ def main():
         for t, r in enumerate(rows):
             if r[0] > 1.5 * sorted(ms)[len(ms) // 2] or t % 16 == 0:
                 print(f'  t={t:2d} {r[0]:.3f} ms  lane max: events {r[1]} toi calls {r[2]} pos iters {r[3]};'
-                      f'  totals: events {r[4]} toi calls {r[5]}; general envs {r[6]}; lane max us: pre-test {r[7][0]:.1f} '
-                      f'toi {r[7][1]:.1f} min+collide {r[7][2]:.1f} position {r[7][3]:.1f} velocity {r[7][4]:.1f}', flush=True)
+                      f'  totals: events {r[4]} toi calls {r[5]}; general envs {r[6]}; lane max us: '
+                      f'toi {r[7][0]:.1f} min+collide+gather {r[7][1]:.1f} position {r[7][2]:.1f} velocity {r[7][3]:.1f} integrate {r[7][4]:.1f}', flush=True)
 
 
 if __name__ == '__main__':

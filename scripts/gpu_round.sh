@@ -21,6 +21,9 @@ for step in "$@"; do
     bench)
       cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_driver.log 2>&1 || exit $?
       cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $? ;;
+    benchq)
+      cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $?
+      cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver.log 2>&1 || exit $? ;;
     env)
       cd $R && timeout -k 10 200 python bench.py --mode env --no-cpu-baseline > $O/bench_env.log 2>&1 || exit $?
       cd $R && timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_ffa.log 2>&1 || exit $?

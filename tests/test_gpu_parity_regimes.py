@@ -203,7 +203,7 @@ def test_invalid_actions_counted_and_rejected():
     env.close()
 
 
-@pytest.mark.parametrize('name', ['c3_2v2_script_s3', 'nonomni_lastalive_s7', 'c5_ffa4_script_s5'])
+@pytest.mark.parametrize('name', ['c3_2v2_script_s3.npz', 'nonomni_lastalive_s7.npz', 'c5_ffa4_script_s5.npz'])
 def test_facade_dict_obs_match_golden(name):
     """The reference-shaped MaSurvival facade returns the fixture's dict keys,
     and each key's array equals the fixture row sliced by the layout."""
