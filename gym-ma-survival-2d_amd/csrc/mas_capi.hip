@@ -326,6 +326,7 @@ static void build_layout(mas_handle* h)
         {"heal_slot_mask", 1, 1, 0, H > 0, &P.o_hsm},
         {"heals", 2, H, 2, H > 0, &P.o_heal},
         {"heals_mask", 1, H, 0, H > 0, &P.o_healm},
+        {"lidars", 1, c.lidar_n_lasers, 0, c.lidar_n_lasers > 0, &P.o_lid},
         {"others", 2, A - 1, as_, true, &P.o_oth},
         {"others_mask", 1, A - 1, 0, true, &P.o_othm},
         {"zone", 1, 6, 0, true, &P.o_zone},
@@ -452,6 +453,11 @@ static int build_params(mas_handle* h)
         V2 vs[4] = {mk(0.0f, 0.0f), left, center, right};
         P.cone = poly_set4(vs);
     }
+    // Lidars._endpoints (simulation.py:385-392): per-laser angle offsets, float64
+    P.n_lasers = c.lidar_n_lasers;
+    P.lid_depth = c.lidar_depth;
+    for (int k = 0; k < P.n_lasers; ++k)
+        P.lid_off[k] = (double)k * (c.lidar_fov / (double)(P.n_lasers - 1)) - c.lidar_fov / 2.0;
     build_layout(h);
     return MAS_OK;
 }
@@ -471,6 +477,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
         return fail(MAS_ERR_INVALID_ARG, "mas_create: spawn grid too large (>256 cells) or too small for the spawns");
     if (c.zone_phases < 1 || c.zone_n_radii + 1 > kMaxPhases || c.zone_phases > c.zone_n_radii + 1)
         return fail(MAS_ERR_INVALID_ARG, "mas_create: unsupported safe-zone phases");
+    if (c.lidar_n_lasers != 0 && (c.lidar_n_lasers < 2 || c.lidar_n_lasers > MAS_MAX_LASERS))
+        return fail(MAS_ERR_INVALID_ARG, "mas_create: lidar n_lasers must be 0 or in [2, MAS_MAX_LASERS]");
     mas_handle* h = new (std::nothrow) mas_handle();
     if (!h) return fail(MAS_ERR_OOM, "mas_create: out of host memory");
     h->cfg = c;

@@ -30,6 +30,7 @@ constexpr int kItemNone = 0, kItemHeal = 1, kItemBox = 2;
 constexpr int kNumWalls = 4;
 constexpr int kMaxPhases = 9;   // zone radii incl. the appended 0
 constexpr int kStats = 19;      // MAS_STATS_WIDTH
+constexpr int kMaxLasers = 32;  // MAS_MAX_LASERS
 
 template <int AM_, int HM_, int BM_, int SM_, int KC_>
 struct Cap {
@@ -72,7 +73,12 @@ struct Params {
     Poly4 cone;
     V2 wall_lo[kNumWalls], wall_hi[kNumWalls];  // world AABBs of the walls (ray-cast culling)
     // observation key offsets (sorted-key layout); -1 when absent
-    int o_agent, o_bi, o_bim, o_bs, o_bsm, o_box, o_boxm, o_hs, o_hsm, o_heal, o_healm, o_oth, o_othm, o_zone;
+    int o_agent, o_bi, o_bim, o_bs, o_bsm, o_box, o_boxm, o_hs, o_hsm, o_heal, o_healm, o_oth, o_othm, o_zone, o_lid;
+    // Lidars (simulation.py:357-392; 0 lasers = off): laser k's angle offset
+    // i*(fov/(n_lasers-1)) - fov/2. in float64 as Python computes it (:388)
+    int n_lasers;
+    float lid_depth;
+    double lid_off[kMaxLasers];
     int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
     int* phys_count;  // number of them
     uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)

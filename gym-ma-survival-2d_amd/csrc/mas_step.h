@@ -59,9 +59,9 @@ __device__ __forceinline__ V2 body_pos(const EnvL<C>& L, const Params& P, int k)
 // closest fixture over ALL fixtures (sensors included); returns the body
 // index or -1.  A report at fraction 0 ends the traversal (b2DynamicTree).
 template <class C>
-__device__ __forceinline__ int ray_cast(const EnvL<C>& L, const Params& P, V2 p1, V2 p2)
+__device__ __forceinline__ int ray_cast(const EnvL<C>& L, const Params& P, V2 p1, V2 p2, float& maxf)
 {
-    float maxf = 1.0f;
+    maxf = 1.0f;
     int hit = -1;
     bool stop = false;
 #pragma unroll
@@ -96,6 +96,30 @@ __device__ __forceinline__ int ray_cast(const EnvL<C>& L, const Params& P, V2 p1
         if (f >= 0.0f) { hit = BIdx<C>::agent + i; maxf = f; stop = maxf == 0.0f; }
     }
     return hit;
+}
+
+template <class C>
+__device__ __forceinline__ int ray_cast(const EnvL<C>& L, const Params& P, V2 p1, V2 p2)
+{
+    float f;
+    return ray_cast(L, P, p1, p2, f);
+}
+
+// Lidars._update (simulation.py:377-392) for laser k of agent i: the
+// Lidars module runs last in the agents group, so its scans see this step's
+// final world -- the state k_obs reads.  The 'lidars' key (DESIGN.md
+// section 2) holds the laser's relative depth (laser_scan :431-439), 1 when
+// nothing is hit, 0 for a dead agent.
+template <class C>
+__device__ __forceinline__ float lidar_depth(const EnvL<C>& L, const Params& P, int i, int k)
+{
+    if (!bit(L.alive_m, i)) return 0.0f;
+    const V2 org = sel(L.c, i);
+    // Python float64: i*(fov/(n_lasers-1)) - fov/2. + orientation (:388-389)
+    const float ang = (float)(P.lid_off[k] + (double)sel(L.a, i));
+    const V2 end = add(org, from_polar(P.lid_depth, ang));
+    float f;
+    return ray_cast(L, P, org, end, f) < 0 ? 1.0f : f;
 }
 
 // Fixture table: per-lane LDS copy of what a ray test needs by runtime body
@@ -681,6 +705,12 @@ __device__ __forceinline__ void write_obs_row(const EnvL<C>& L, const Params& P,
                 else m = (present && alive && ((seen_of(L, BIdx<C>::bitem + b) >> pp) & 1u)) ? 0.0f : 1.0f;
                 row(P.o_bim + b, m);
             }
+        }
+        // lidars: zeros here; k_lidar (one lane per ray) writes the columns
+        // after k_obs, so this row writer keeps its register budget
+        if (P.n_lasers > 0 && row.want(P.o_lid, P.n_lasers)) {
+#pragma unroll 1
+            for (int k = 0; k < P.n_lasers; ++k) row(P.o_lid + k, 0.0f);
         }
         // usable inventory slots (:620-654)
         int lastmeta = 0;

@@ -8,8 +8,11 @@ from collections import OrderedDict
 from typing import Dict, Tuple
 
 
-def obs_key_shapes(n_agents: int, n_heals: int, n_boxes: int, has_teams: bool) -> 'OrderedDict[str, Tuple[int, ...]]':
-    """Per-agent sub-array shape for every observation key, in Dict order."""
+def obs_key_shapes(n_agents: int, n_heals: int, n_boxes: int, has_teams: bool,
+                   n_lasers: int = 0) -> 'OrderedDict[str, Tuple[int, ...]]':
+    """Per-agent sub-array shape for every observation key, in Dict order.
+    ``n_lasers`` > 0 adds the opt-in 'lidars' key (one relative depth per
+    laser of the Lidars module, simulation.py:357-392)."""
     agent_size = 1 + 1 + 3 + 3 + (1 if has_teams else 0)
     d: Dict[str, Tuple[int, ...]] = {
         'agent': (agent_size,),
@@ -29,14 +32,16 @@ def obs_key_shapes(n_agents: int, n_heals: int, n_boxes: int, has_teams: bool) -
         d['box_items_mask'] = (n_boxes,)
         d['box_slot'] = (1, 8)
         d['box_slot_mask'] = (1,)
+    if n_lasers > 0:
+        d['lidars'] = (n_lasers,)
     return OrderedDict(sorted(d.items()))
 
 
-def obs_layout(n_agents: int, n_heals: int, n_boxes: int, has_teams: bool):
+def obs_layout(n_agents: int, n_heals: int, n_boxes: int, has_teams: bool, n_lasers: int = 0):
     """Returns (obs_dim, {key: (offset, per-agent shape)})."""
     off = 0
     out = OrderedDict()
-    for k, shp in obs_key_shapes(n_agents, n_heals, n_boxes, has_teams).items():
+    for k, shp in obs_key_shapes(n_agents, n_heals, n_boxes, has_teams, n_lasers).items():
         size = 1
         for s in shp:
             size *= s

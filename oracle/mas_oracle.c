@@ -1428,6 +1428,10 @@ ora_env* ora_env_create(const mas_config* cfg, char* err, int32_t errlen)
         if (err) snprintf(err, errlen, "oracle: unsupported config sizes");
         return NULL;
     }
+    if (cfg->lidar_n_lasers != 0 && (cfg->lidar_n_lasers < 2 || cfg->lidar_n_lasers > MAS_MAX_LASERS)) {
+        if (err) snprintf(err, errlen, "oracle: lidar n_lasers must be 0 or in [2, %d]", MAS_MAX_LASERS);
+        return NULL;
+    }
     if (cfg->n_agents + cfg->n_heals + cfg->n_boxes > cfg->grid_size * cfg->grid_size) {
         if (err) snprintf(err, errlen, "oracle: more spawns than grid cells (IndexError semantics.py:77)");
         return NULL;
@@ -1440,7 +1444,7 @@ ora_env* ora_env_create(const mas_config* cfg, char* err, int32_t errlen)
     e->as_ = 8 + (cfg->teams ? 1 : 0);
     e->melee_cd = cfg->melee_cooldown;
     int A = e->A, H = e->H, B = e->B;
-    e->D = e->as_ * A + 6 + (A - 1) + (H > 0 ? 3 * H + 2 : 0) + (B > 0 ? 23 * B + 9 : 0);
+    e->D = e->as_ * A + 6 + (A - 1) + (H > 0 ? 3 * H + 2 : 0) + (B > 0 ? 23 * B + 9 : 0) + cfg->lidar_n_lasers;
     e->agent_r = (float)(cfg->agent_size / 2.0);
     e->heal_r = (float)(cfg->heal_size / 2.0);
     e->bitem_r = (float)(cfg->box_item_size / 2.0);
@@ -1598,43 +1602,51 @@ static void box_change_health(ora_env* e, int b, int delta, int cause)
 /* ---- fixture iteration in canonical order (groups in dict order) ---- */
 typedef struct { int kind, idx; } bref;
 
-/* simulation.py:431-439 laser_scan + LaserRayCastCallback (:471-484) */
-static bref ray_cast(const ora_env* e, v2 p1, v2 p2)
+/* simulation.py:431-439 laser_scan + LaserRayCastCallback (:471-484): the
+ * last reported fixture and its fraction (relative_depth) */
+static bref ray_cast_f(const ora_env* e, v2 p1, v2 p2, float* frac)
 {
     bref hit = {-1, -1};
     float maxf = 1.0f, f;
+    *frac = 1.0f;
     for (int b = 0; b < e->nbox; ++b) {
         if (ora_ray_poly(&e->box[b].shape, e->box[b].pos, e->box[b].q, p1, p2, maxf, &f)) {
-            hit.kind = K_BOX; hit.idx = b; maxf = f;
+            hit.kind = K_BOX; hit.idx = b; maxf = f; *frac = f;
             if (maxf == 0.0f) return hit;
         }
     }
     for (int b = 0; b < e->nbi; ++b) {
         if (ora_ray_circle(e->bitem_r, e->bi[b].pos, p1, p2, maxf, &f)) {
-            hit.kind = K_BITEM; hit.idx = b; maxf = f;
+            hit.kind = K_BITEM; hit.idx = b; maxf = f; *frac = f;
             if (maxf == 0.0f) return hit;
         }
     }
     for (int h = 0; h < e->nheal; ++h) {
         if (ora_ray_circle(e->heal_r, e->heal[h].pos, p1, p2, maxf, &f)) {
-            hit.kind = K_HEAL; hit.idx = h; maxf = f;
+            hit.kind = K_HEAL; hit.idx = h; maxf = f; *frac = f;
             if (maxf == 0.0f) return hit;
         }
     }
     for (int k = 0; k < NWALLS; ++k) {
         if (ora_ray_poly(&e->wall_poly, e->wall_pos[k], e->wall_q[k], p1, p2, maxf, &f)) {
-            hit.kind = K_WALL; hit.idx = k; maxf = f;
+            hit.kind = K_WALL; hit.idx = k; maxf = f; *frac = f;
             if (maxf == 0.0f) return hit;
         }
     }
     for (int i = 0; i < e->A; ++i) {
         if (!e->alive[i]) continue;
         if (ora_ray_circle(e->agent_r, e->w.c[i], p1, p2, maxf, &f)) {
-            hit.kind = K_AGENT; hit.idx = i; maxf = f;
+            hit.kind = K_AGENT; hit.idx = i; maxf = f; *frac = f;
             if (maxf == 0.0f) return hit;
         }
     }
     return hit;
+}
+
+static bref ray_cast(const ora_env* e, v2 p1, v2 p2)
+{
+    float f;
+    return ray_cast_f(e, p1, p2, &f);
 }
 
 static v2 body_pos(const ora_env* e, bref r)
@@ -1730,6 +1742,8 @@ static void write_obs(ora_env* e, float* obs)
         o_heal = off; off += 2 * H;
         o_healm = off; off += H;
     }
+    const int NL = e->cfg.lidar_n_lasers;
+    int o_lid = off; off += NL;
     int o_oth = off; off += (A - 1) * as_;
     int o_othm = off; off += A - 1;
     int o_zone = off; off += 6;
@@ -1823,6 +1837,22 @@ static void write_obs(ora_env* e, float* obs)
                 if (e->cfg.omniscient) m = b < e->nbi ? 0.0f : 1.0f;
                 else m = (b < e->nbi && use_seen && seen_has(e, p, e->bi[b].serial)) ? 0.0f : 1.0f;
                 row[o_bim + b] = m;
+            }
+        }
+        /* lidars: Lidars._update (simulation.py:377-392) as the last agents
+         * module, so its scans see this step's final world; the 'lidars' key
+         * (this build's extension) holds each laser's
+         * relative depth, 1 when the ray hits nothing, 0 for a dead agent */
+        if (NL > 0 && e->alive[i]) {
+            v2 origin = e->w.c[i];
+            for (int k = 0; k < NL; ++k) {
+                /* Python float64: i*(fov/(n_lasers-1)) - fov/2. + orientation (:388-389) */
+                double ang = (double)k * (e->cfg.lidar_fov / (double)(NL - 1)) - e->cfg.lidar_fov / 2.0;
+                ang += (double)e->w.a[i];
+                v2 end = vadd(origin, from_polar(e->cfg.lidar_depth, (float)ang));
+                float f;
+                bref hit = ray_cast_f(e, origin, end, &f);
+                row[o_lid + k] = hit.kind < 0 ? 1.0f : f;
             }
         }
         /* inventory slots (:620-654) */

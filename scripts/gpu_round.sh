@@ -38,6 +38,9 @@ for step in "$@"; do
         -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || exit $?
       cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mas::k_" --output-format csv \
         -d $O/pmc_write -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_write.log 2>&1 || exit $? ;;
+    profgen)
+      cd $R && timeout -k 10 300 python -u profiles/prof_toi.py 65536 4 > $O/prof_toi.log 2>&1 || exit $?
+      cd $R && timeout -k 10 300 python -u profiles/prof_general.py 65536 20 --ppo > $O/prof_general.log 2>&1 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"

@@ -145,13 +145,45 @@ def collector_actions(obs, rng, A, teams):
     return tuple(acts)
 
 
+def lidar_obs(env, lidars):
+    """The 'lidars' observation key of this build: the
+    reference's own Lidars module (simulation.py:357-392) computes the scans;
+    agent i's row holds its lasers' relative depths (laser_scan :431-439), 1
+    where nothing is hit, zeros for a dead agent (no body).  Lidars is the
+    last agents module, so scans[k] belongs to agents.bodies[k]."""
+    agents = env.simulation.groups['agents']
+    sim = sys.modules['masurvival.simulation']
+    indexed = agents.get(sim.IndexBodies)[0].bodies
+    out = np.zeros((env.n_agents, lidars.n_lasers), dtype=np.float32)
+    for i, body in enumerate(indexed):
+        if body is None:
+            continue
+        k = agents.bodies.index(body)
+        out[i] = [1.0 if s is None else s[1] for s in lidars.scans[k]]
+    return out
+
+
 def run_episode(mod, name, config, env_seed, act_seed, max_steps, p_script):
+    lid_cfg = None
+    if config is not None and 'lidars' in config:
+        # the reference env has no 'lidars' config key (BaseEnv merge raises
+        # KeyError); its Lidars module is attached as the last agents module
+        config = dict(config)
+        lid_cfg = config.pop('lidars')
     env = mod.MaSurvival(config=copy.deepcopy(config) if config is not None else None)
+    lidars = None
+    if lid_cfg is not None:
+        sim = sys.modules['masurvival.simulation']
+        lidars = sim.Lidars(**lid_cfg)
+        env.simulation.groups['agents'].modules.append(lidars)
+        config = dict(config, lidars=lid_cfg)
     groups = env.simulation.groups
     Box2D.CANONICAL_GROUPS[:] = list(groups.values())
     Box2D.STATIC_GROUPS[:] = [groups['walls'], groups['boxes']]
     env.np_random = np.random.default_rng(env_seed)
     obs = env.reset()
+    if lidars is not None:
+        obs['lidars'] = lidar_obs(env, lidars)
     flat0, keys = flatten_obs(obs)
     A = env.n_agents
     rng = np.random.default_rng(act_seed)
@@ -165,6 +197,8 @@ def run_episode(mod, name, config, env_seed, act_seed, max_steps, p_script):
         else:
             acts = scripted_actions(obs, rng, A, p_script, env.has_teams)
         obs, rew, done, info = env.step(acts)
+        if lidars is not None:
+            obs['lidars'] = lidar_obs(env, lidars)
         obs_l.append(flatten_obs(obs)[0])
         act_l.append(np.stack(acts).astype(np.int8))
         rew_l.append(np.asarray(rew, dtype=np.float32))
@@ -236,6 +270,21 @@ EPISODES = [
         'boxes': {'reset_spawns': {'n_boxes': 0, 'box_size': 1}, 'ownership': False,
                   'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20},
         'melee': MELEE}, 8, 108, 300, 0.5),
+    # Lidars (simulation.py:357-392), opt-in 'lidars' key: 2v2 fights, FFA4
+    # with heals + randomized boxes (rays hit every body kind), and the
+    # minimum of two lasers with rays longer than the room
+    ('lidars_2v2_s12', {'agents': {'n_agents': 4, 'agent_size': 1}, 'teams': {'twoteams': True}, 'melee': MELEE,
+                        'lidars': {'n_lasers': 8, 'fov': 0.5 * math.pi, 'depth': 6}}, 12, 112, 600, 0.8),
+    ('lidars_ffa4_s13', {
+        'agents': {'n_agents': 4, 'agent_size': 1},
+        'spawn_grid': {'grid_size': 6, 'floor_size': 14},
+        'heals': {'reset_spawns': {'n_items': 8, 'item_size': 0.5}, 'heal': {'healing': 50}},
+        'boxes': {'reset_spawns': {'n_boxes': 8, 'box_size': 1}, 'ownership': False,
+                  'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20,
+                  'randomized_shape': {'avg_w': 1.0, 'std_w': 0.5, 'avg_h': 1.0, 'std_h': 0.5}},
+        'melee': MELEE, 'lidars': {'n_lasers': 16, 'fov': 2.0 * math.pi * 15 / 16, 'depth': 5.5}},
+     13, 113, 500, -2),
+    ('lidars_1v1_s14', {'melee': MELEE, 'lidars': {'n_lasers': 2, 'fov': 0.3, 'depth': 30}}, 14, 114, 400, 0.6),
 ]
 
 

@@ -54,3 +54,18 @@ def test_split_obs_roundtrip():
     back = np.concatenate([parts[k].reshape(4, -1) for k in lay], axis=1)
     assert np.array_equal(back, flat)
     assert parts['others'].shape == (4, 3, 9)
+
+
+def test_lidars_key_is_opt_in_and_sorted():
+    base = ResolvedConfig(C3_CONFIG)
+    d0, lay0 = obs_layout(base.n_agents, base.n_heals, base.n_boxes, base.has_teams)
+    assert 'lidars' not in lay0 and base.lidars is None
+    rc = ResolvedConfig(dict(C3_CONFIG, lidars={'n_lasers': 8, 'fov': 1.5, 'depth': 6}))
+    s = rc.to_struct()
+    assert (s.lidar_n_lasers, s.lidar_fov, s.lidar_depth) == (8, 1.5, 6.0)
+    d, lay = obs_layout(rc.n_agents, rc.n_heals, rc.n_boxes, rc.has_teams, 8)
+    assert d == d0 + 8 and list(lay) == sorted(lay)
+    assert lay['lidars'] == (lay0['others'][0], (8,))
+    for bad in (1, 33):
+        with pytest.raises(ValueError):
+            ResolvedConfig(dict(C3_CONFIG, lidars={'n_lasers': bad, 'fov': 1.0, 'depth': 5}))
