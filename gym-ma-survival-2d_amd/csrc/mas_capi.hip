@@ -417,6 +417,7 @@ static int build_params(mas_handle* h)
         P.inv_mass = 1.0f / m;
         bI -= m * 0.0f;
         P.inv_I = 1.0f / bI;
+        P.inv_mass_rcp = 1.0 / (double)P.inv_mass;
     }
     P.lin_damp = 0.8f;  // simulation.py:114 default_damping
     P.ang_damp = 0.8f;

@@ -65,6 +65,7 @@ struct Params {
     double floor_size;
     int grid_size;
     float inv_mass, inv_I, lin_damp, ang_damp;
+    double inv_mass_rcp;  // 1 / (double)inv_mass (div_by_m, mas_physics.h)
     int w_cont;  // first state word of the contact memory (kGCont)
     Poly4 wall_poly;
     V2 wall_pos[kNumWalls];

@@ -178,19 +178,28 @@ MAS_HD float pc_solve_aa(V2& cA, float& aA, V2& cB, float& aB, float r, float m,
     return sep;
 }
 
-MAS_HD float pc_solve_as(V2 sp, Rot sq, V2 ln, V2 lp, V2& cB, float& aB, float r, float m, float I, float baum)
+// (-Cc) / K of an agent-vs-static position constraint.  There K = mA + m +
+// iA rnA^2 + I rnB^2 with mA = iA = 0 and rB = point - cB = cB - cB = 0, so K
+// is exactly m (the agent's inverse mass) for finite operands, and K > 0.
+// The quotient is one float64 multiply by rm = 1 / (double)m, rounded once to
+// float: its relative error is below 2^-52, while a quotient of two floats
+// lies at least 2^-49 (relative) away from any float rounding midpoint, so
+// the rounding is the correctly rounded x / m -- the same bits as the IEEE
+// division, without its 12-instruction dependent chain (the hot loop of the
+// TOI position iterations).
+MAS_HD float div_by_m(float x, double rm) { return (float)((double)x * rm); }
+
+MAS_HD float pc_solve_as(V2 sp, Rot sq, V2 ln, V2 lp, V2& cB, float& aB, float r, float m, float I, float baum,
+                         double rm)
 {
     V2 normal = rmul(sq, ln);
     V2 planePoint = xmul(sp, sq, lp);
     V2 clip = cB;
     float sep = dot(sub(clip, planePoint), normal) - kPolyRadius - r;
     V2 point = clip;
-    V2 rA = sub(point, sp), rB = sub(point, cB);
+    V2 rB = sub(point, cB);
     float Cc = clamp_b2(baum * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
-    const float mA = 0.0f, iA = 0.0f;
-    float rnA = cross(rA, normal), rnB = cross(rB, normal);
-    float K = mA + m + iA * rnA * rnA + I * rnB * rnB;
-    float imp = K > 0.0f ? -Cc / K : 0.0f;
+    float imp = div_by_m(-Cc, rm);  // K == m: see div_by_m
     V2 Pp = scl(imp, normal);
     cB = add(cB, scl(m, Pp));
     aB += I * cross(rB, Pp);
@@ -506,7 +515,7 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const C
                     static_pq(L, P, js, sp, sq);
                     V2 cB = sel(L.c, i);
                     float aB = sel(L.a, i);
-                    sep = pc_solve_as(sp, sq, sl.ln[q], sl.lp[q], cB, aB, P.agent_r, m, I, kBaumgarte);
+                    sep = pc_solve_as(sp, sq, sl.ln[q], sl.lp[q], cB, aB, P.agent_r, m, I, kBaumgarte, P.inv_mass_rcp);
                     put(L.c, i, cB); put(L.a, i, aB);
                 }
 #pragma unroll
@@ -542,7 +551,7 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const C
                     collide_pc(g.poly, g.p, g.q, sel(S.c0, i), kPolyRadius, P.agent_r, ln, lp);
                     V2 cB = sel(L.c, i);
                     float aB = sel(L.a, i);
-                    float sep = pc_solve_as(g.p, g.q, ln, lp, cB, aB, P.agent_r, m, I, kBaumgarte);
+                    float sep = pc_solve_as(g.p, g.q, ln, lp, cB, aB, P.agent_r, m, I, kBaumgarte, P.inv_mass_rcp);
                     put(L.c, i, cB); put(L.a, i, aB);
                     put(minsep, root, fmin_b2(sel(minsep, root), sep));
                 }
@@ -1157,12 +1166,12 @@ __device__ __forceinline__ int toi_agent(EnvL<C>& L, const Params& P, const KT& 
             ++npos;
 #endif
             float minsep = 0.0f;
-            minsep = fmin_b2(minsep, pc_solve_as(gm.p, gm.q, lnm, lpm, cB, aB, P.agent_r, m, Ii, kToiBaumgarte));
+            minsep = fmin_b2(minsep, pc_solve_as(gm.p, gm.q, lnm, lpm, cB, aB, P.agent_r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
 #pragma unroll
             for (int s = 0; s < C::NS; ++s) {
                 if (!bit(isl, s)) continue;
                 StaticG g = static_geom(L, P, s);
-                minsep = fmin_b2(minsep, pc_solve_as(g.p, g.q, iln[s], ilp[s], cB, aB, P.agent_r, m, Ii, kToiBaumgarte));
+                minsep = fmin_b2(minsep, pc_solve_as(g.p, g.q, iln[s], ilp[s], cB, aB, P.agent_r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
             }
             if (minsep >= -1.5f * kLinearSlop) break;
         }
@@ -1262,18 +1271,15 @@ __device__ __forceinline__ T gshfl(T v, int src)
 
 // pc_solve_as / vc_init_as with the contact's normal and plane point given
 // (rmul(sq, ln), xmul(sp, sq, lp) hoisted by the caller): identical ops
-MAS_HD float pc_solve_as_h(V2 normal, V2 planePoint, V2 sp, V2& cB, float& aB, float r, float m, float I,
-                           float baum)
+MAS_HD float pc_solve_as_h(V2 normal, V2 planePoint, V2& cB, float& aB, float r, float m, float I, float baum,
+                           double rm)
 {
     V2 clip = cB;
     float sep = dot(sub(clip, planePoint), normal) - kPolyRadius - r;
     V2 point = clip;
-    V2 rA = sub(point, sp), rB = sub(point, cB);
+    V2 rB = sub(point, cB);
     float Cc = clamp_b2(baum * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
-    const float mA = 0.0f, iA = 0.0f;
-    float rnA = cross(rA, normal), rnB = cross(rB, normal);
-    float K = mA + m + iA * rnA * rnA + I * rnB * rnB;
-    float imp = K > 0.0f ? -Cc / K : 0.0f;
+    float imp = div_by_m(-Cc, rm);  // K == m: see div_by_m
     V2 Pp = scl(imp, normal);
     cB = add(cB, scl(m, Pp));
     aB += I * cross(rB, Pp);
@@ -1451,12 +1457,12 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
             ++npos;
 #endif
             float minsep = 0.0f;
-            minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, sm, cB, aB, r, m, Ii, kToiBaumgarte));
+            minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
 #pragma unroll
             for (int q = 0; q < C::NS; ++q) {
                 if (!bit(isl, q) || q == minS) continue;
-                minsep = fmin_b2(minsep, pc_solve_as_h(nq[q], pq[q], static_pos(L, P, q), cB, aB, r, m, Ii,
-                                                       kToiBaumgarte));
+                minsep = fmin_b2(minsep, pc_solve_as_h(nq[q], pq[q], cB, aB, r, m, Ii, kToiBaumgarte,
+                                                       P.inv_mass_rcp));
             }
             if (minsep >= -1.5f * kLinearSlop) break;
         }
