@@ -1437,66 +1437,115 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
             touch = t;
         }
         const uint32_t isl = (uint32_t)((__ballot(mine && touch) & gmask) >> base);
-        // (5) constraint data of every island contact, once per event
+        // (5) constraint data of every island contact, once per event: the
+        // min contact, then the agent's other touching contacts in static
+        // order in KT compact slots (gathered from their lanes); more than
+        // KT (rare) takes the masked loop over every static
         const V2 nrm = rmul(g.q, ln), ppt = xmul(g.p, g.q, lp);
         const V2 nm = mk(gshfl<G>(nrm.x, minS), gshfl<G>(nrm.y, minS));
         const V2 pm = mk(gshfl<G>(ppt.x, minS), gshfl<G>(ppt.y, minS));
         const V2 sm = mk(gshfl<G>(g.p.x, minS), gshfl<G>(g.p.y, minS));
-        V2 nq[C::NS], pq[C::NS];
+        constexpr int KT = 2;
+        uint32_t rest = isl & ~(1u << minS);
+        const int nsl = __builtin_popcount(rest);
+        V2 sn[KT], spp[KT], ssp[KT];
 #pragma unroll
-        for (int q = 0; q < C::NS; ++q) {
-            nq[q] = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
-            pq[q] = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
+        for (int j = 0; j < KT; ++j) {
+            const int q = rest ? __builtin_ctz(rest) : 0;
+            rest &= rest - 1u;
+            sn[j] = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
+            spp[j] = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
+            ssp[j] = mk(gshfl<G>(g.p.x, q), gshfl<G>(g.p.y, q));
         }
         MAS_GT(1);
-        // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
         V2 cB = sw.c;
         float aB = sw.a;
-        for (int it = 0; it < 20; ++it) {
+        if (nsl <= KT) {
+            // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
+            for (int it = 0; it < 20; ++it) {
 #ifdef MAS_PROFILE
-            ++npos;
+                ++npos;
 #endif
-            float minsep = 0.0f;
-            minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
+                float minsep = 0.0f;
+                minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
+#pragma unroll
+                for (int j = 0; j < KT; ++j)
+                    if (j < nsl)
+                        minsep = fmin_b2(minsep, pc_solve_as_h(sn[j], spp[j], cB, aB, r, m, Ii, kToiBaumgarte,
+                                                               P.inv_mass_rcp));
+                if (minsep >= -1.5f * kLinearSlop) break;
+            }
+            MAS_GT(2);
+            sw.c0 = cB;
+            sw.a0 = aB;
+            // ... then 10 velocity iterations without warm starting
+            VC km = vc_init_as_h(nm, pm, sm, cB, r, m, Ii);
+            VC kq[KT];
+#pragma unroll
+            for (int j = 0; j < KT; ++j) kq[j] = vc_init_as_h(sn[j], spp[j], ssp[j], cB, r, m, Ii);
+            for (int it = 0; it < 10; ++it) {
+                {
+                    V2 vz = mk(0.0f, 0.0f);
+                    float wz = 0.0f;
+                    vc_solve(km, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                }
+#pragma unroll
+                for (int j = 0; j < KT; ++j) {
+                    if (j >= nsl) continue;
+                    V2 vz = mk(0.0f, 0.0f);
+                    float wz = 0.0f;
+                    vc_solve(kq[j], vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                }
+            }
+        } else {
+            V2 nq[C::NS], pq[C::NS];
 #pragma unroll
             for (int q = 0; q < C::NS; ++q) {
-                if (!bit(isl, q) || q == minS) continue;
-                minsep = fmin_b2(minsep, pc_solve_as_h(nq[q], pq[q], cB, aB, r, m, Ii, kToiBaumgarte,
-                                                       P.inv_mass_rcp));
+                nq[q] = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
+                pq[q] = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
             }
-            if (minsep >= -1.5f * kLinearSlop) break;
-        }
-        MAS_GT(2);
-        sw.c0 = cB;
-        sw.a0 = aB;
-        // ... then 10 velocity iterations without warm starting
-        VC km = vc_init_as_h(nm, pm, sm, cB, r, m, Ii);
-        constexpr bool kHoist = C::NS <= 8;  // register budget: hoist every contact's constraint only for small classes
-        VC kq[kHoist ? C::NS : 1];
-        float ni[C::NS], ti[C::NS];
+            for (int it = 0; it < 20; ++it) {
+#ifdef MAS_PROFILE
+                ++npos;
+#endif
+                float minsep = 0.0f;
+                minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
 #pragma unroll
-        for (int q = 0; q < C::NS; ++q) {
-            ni[q] = 0.0f;
-            ti[q] = 0.0f;
-            if (kHoist) kq[kHoist ? q : 0] = vc_init_as_h(nq[q], pq[q], static_pos(L, P, q), cB, r, m, Ii);
-        }
-        for (int it = 0; it < 10; ++it) {
-            {
-                V2 vz = mk(0.0f, 0.0f);
-                float wz = 0.0f;
-                vc_solve(km, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                for (int q = 0; q < C::NS; ++q) {
+                    if (!bit(isl, q) || q == minS) continue;
+                    minsep = fmin_b2(minsep, pc_solve_as_h(nq[q], pq[q], cB, aB, r, m, Ii, kToiBaumgarte,
+                                                           P.inv_mass_rcp));
+                }
+                if (minsep >= -1.5f * kLinearSlop) break;
             }
+            MAS_GT(2);
+            sw.c0 = cB;
+            sw.a0 = aB;
+            VC km = vc_init_as_h(nm, pm, sm, cB, r, m, Ii);
+            float ni[C::NS], ti[C::NS];
 #pragma unroll
             for (int q = 0; q < C::NS; ++q) {
-                if (!bit(isl, q) || q == minS) continue;
-                VC k = kHoist ? kq[kHoist ? q : 0] : vc_init_as_h(nq[q], pq[q], static_pos(L, P, q), cB, r, m, Ii);
-                k.ni = ni[q];
-                k.ti = ti[q];
-                V2 vz = mk(0.0f, 0.0f);
-                float wz = 0.0f;
-                vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
-                ni[q] = k.ni;
-                ti[q] = k.ti;
+                ni[q] = 0.0f;
+                ti[q] = 0.0f;
+            }
+            for (int it = 0; it < 10; ++it) {
+                {
+                    V2 vz = mk(0.0f, 0.0f);
+                    float wz = 0.0f;
+                    vc_solve(km, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                }
+#pragma unroll
+                for (int q = 0; q < C::NS; ++q) {
+                    if (!bit(isl, q) || q == minS) continue;
+                    VC k = vc_init_as_h(nq[q], pq[q], static_pos(L, P, q), cB, r, m, Ii);
+                    k.ni = ni[q];
+                    k.ti = ti[q];
+                    V2 vz = mk(0.0f, 0.0f);
+                    float wz = 0.0f;
+                    vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
+                    ni[q] = k.ni;
+                    ti[q] = k.ti;
+                }
             }
         }
         MAS_GT(3);
