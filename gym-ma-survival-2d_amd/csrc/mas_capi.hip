@@ -299,7 +299,7 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
-    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count
+    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count + [1] k_gen queue
     uint8_t* gen_flag;  // [N] env left the fast path this step
     float* sweep;
     mas_obs_layout layout;
@@ -514,8 +514,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
     h->P.prof = nullptr;
     h->phys = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 2) * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 2) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 3) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 3) * sizeof(int));
     h->sweep = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * 8 * sizeof(float));
     h->P.sweep = h->sweep;
@@ -526,6 +526,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.phys_list = h->phys;
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
     h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
+    h->P.gen_next = h->phys ? h->phys + n_envs + 2 : nullptr;
     h->P.toi_diag = nullptr;
 #ifdef MAS_PROFILE
     if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));

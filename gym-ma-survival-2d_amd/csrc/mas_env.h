@@ -82,6 +82,7 @@ struct Params {
     double lid_off[kMaxLasers];
     int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
     int* phys_count;  // number of them
+    int* gen_next;    // k_gen work queue: next chunk of the list (reset by k_pre)
     uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)
     float* sweep;     // [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
     int* toi_diag;    // test diagnostics (mas_debug_set_toi_counter): per env, TOI events + 65536 per capped SolveTOI
@@ -186,6 +187,12 @@ struct ContGlbStore {  // the kGCont words of the HBM image (rare paths)
     int64_t N, e;
     int w0;
     MAS_HD uint32_t& w(int k) const { return st[state_index(w0 + k, e, N)]; }
+};
+
+template <class C, int S>
+struct ContEnvLds {  // one env's words in LDS shared by the env's lanes, [word][S] (S envs per workgroup)
+    uint32_t* u;     // this env's column
+    MAS_HD uint32_t& w(int k) const { return u[k * S]; }
 };
 
 template <class C, class S = ContLdsStore<C>>

@@ -254,14 +254,13 @@ __device__ __forceinline__ void static_pq(const EnvL<C>& L, const Params& P, int
         if (s == kNumWalls + b) { sp = opq(L.bp[b]); sq = kIdRot; }
 }
 
-template <class C>
-__device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const Cont<C>& K, StepScratch<C>& S, float h,
-                                            float dtRatio)
+// Islands over touching agent-agent contacts (Box2D DFS; statics do not
+// propagate): label[i] = the smallest agent index of i's island; returns the
+// solved agents (members of islands with an awake member).
+template <class C, class KT>
+__device__ __forceinline__ uint32_t island_labels(const EnvL<C>& L, const KT& K, int (&label)[C::AM])
 {
     constexpr int AM = C::AM;
-    const float m = P.inv_mass, I = P.inv_I;
-    // islands over touching agent-agent contacts (Box2D DFS; statics do not propagate)
-    int label[AM];
 #pragma unroll
     for (int i = 0; i < AM; ++i) label[i] = i;
     // (agent-agent contacts are rare: the whole wave skips the propagation
@@ -273,8 +272,6 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const C
         for (int i = 0; i < AM; ++i)
 #pragma unroll
             for (int j = i + 1; j < AM; ++j) {
-                constexpr int dummy = 0;
-                (void)dummy;
                 int p = aa_index<AM>(i, j);
                 if (bit(L.alive_m, i) && bit(L.alive_m, j) && bit(K.aat(), p)) {
                     int l = label[i] < label[j] ? label[i] : label[j];
@@ -283,7 +280,6 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const C
                 }
             }
     }
-    // solved agents: members of islands with an awake member
     uint32_t solved = 0;
 #pragma unroll
     for (int i = 0; i < AM; ++i) {
@@ -293,6 +289,20 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const C
             if (label[j] == label[i] && bit(L.alive_m, j) && bit(L.awake_m, j)) any = true;
         if (bit(L.alive_m, i) && any) solved |= 1u << i;
     }
+    return solved;
+}
+
+// b2Island::Solve over the solved agents, restricted to `only` (k_gen: one
+// island per call, its root's lane; islands share no body, so solving them
+// apart is solving them together)
+template <class C, class KT>
+__device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const KT& K, StepScratch<C>& S, float h,
+                                            float dtRatio, uint32_t only = ~0u)
+{
+    constexpr int AM = C::AM;
+    const float m = P.inv_mass, I = P.inv_I;
+    int label[AM];
+    const uint32_t solved = island_labels(L, K, label) & only;
     if (solved == 0) return;
 #pragma unroll
     for (int i = 0; i < AM; ++i)
@@ -1327,10 +1337,9 @@ struct ToiGroupOut {
 // agent's sweep start (b2Sweep c0/a0 of this world step); L: the env after
 // the island solve; K: the contact memory in HBM (impulse resets of this
 // lane's contact are written there); t0: agent I's touching word.
-template <class C, int G>
-__device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const Params& P,
-                                                       const Cont<C, ContGlbStore<C>>& K, int I, int s, V2 c0,
-                                                       float a0, uint32_t t0, float dt)
+template <class C, int G, class KT>
+__device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const Params& P, const KT& K, int I, int s,
+                                                       V2 c0, float a0, uint32_t t0, float dt)
 {
     static_assert(G >= C::NS && G <= 64 && (G & (G - 1)) == 0, "one lane per static");
     const float r = P.agent_r, m = P.inv_mass, Ii = P.inv_I;
@@ -1445,12 +1454,12 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
         const V2 nm = mk(gshfl<G>(nrm.x, minS), gshfl<G>(nrm.y, minS));
         const V2 pm = mk(gshfl<G>(ppt.x, minS), gshfl<G>(ppt.y, minS));
         const V2 sm = mk(gshfl<G>(g.p.x, minS), gshfl<G>(g.p.y, minS));
-        constexpr int KT = 2;
+        constexpr int NSLOT = 2;
         uint32_t rest = isl & ~(1u << minS);
         const int nsl = __builtin_popcount(rest);
-        V2 sn[KT], spp[KT], ssp[KT];
+        V2 sn[NSLOT], spp[NSLOT], ssp[NSLOT];
 #pragma unroll
-        for (int j = 0; j < KT; ++j) {
+        for (int j = 0; j < NSLOT; ++j) {
             const int q = rest ? __builtin_ctz(rest) : 0;
             rest &= rest - 1u;
             sn[j] = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
@@ -1460,7 +1469,7 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
         MAS_GT(1);
         V2 cB = sw.c;
         float aB = sw.a;
-        if (nsl <= KT) {
+        if (nsl <= NSLOT) {
             // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
             for (int it = 0; it < 20; ++it) {
 #ifdef MAS_PROFILE
@@ -1469,7 +1478,7 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                 float minsep = 0.0f;
                 minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
 #pragma unroll
-                for (int j = 0; j < KT; ++j)
+                for (int j = 0; j < NSLOT; ++j)
                     if (j < nsl)
                         minsep = fmin_b2(minsep, pc_solve_as_h(sn[j], spp[j], cB, aB, r, m, Ii, kToiBaumgarte,
                                                                P.inv_mass_rcp));
@@ -1480,9 +1489,9 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
             sw.a0 = aB;
             // ... then 10 velocity iterations without warm starting
             VC km = vc_init_as_h(nm, pm, sm, cB, r, m, Ii);
-            VC kq[KT];
+            VC kq[NSLOT];
 #pragma unroll
-            for (int j = 0; j < KT; ++j) kq[j] = vc_init_as_h(sn[j], spp[j], ssp[j], cB, r, m, Ii);
+            for (int j = 0; j < NSLOT; ++j) kq[j] = vc_init_as_h(sn[j], spp[j], ssp[j], cB, r, m, Ii);
             for (int it = 0; it < 10; ++it) {
                 {
                     V2 vz = mk(0.0f, 0.0f);
@@ -1490,7 +1499,7 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                     vc_solve(km, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
                 }
 #pragma unroll
-                for (int j = 0; j < KT; ++j) {
+                for (int j = 0; j < NSLOT; ++j) {
                     if (j >= nsl) continue;
                     V2 vz = mk(0.0f, 0.0f);
                     float wz = 0.0f;
@@ -1583,6 +1592,182 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
 #endif
 #undef MAS_GT
     return o;
+}
+
+// ---------------------------------------------------------------------------
+// One b2World::Step of the general path on a lane group of the env (k_gen):
+// lane (I, s) = agent I, static s, G lanes per agent.  Same state changes, in
+// the same order per body, as world_step_solve + toi_agent_group:
+//   Collide   agent-agent pairs on every lane (same values; the env's lane 0
+//             writes their memory); agent-static pair (I, s) on its own lane
+//             (b2Contact::Update, impulse reset, wake on a touching change);
+//   Solve     every lane labels the islands; the lane (root, 0) of each
+//             solved island runs b2Island::Solve for that island alone
+//             (islands share no body: solving them apart is solving them
+//             together, in the canonical contact order within each);
+//   SolveTOI  per awake agent on its G lanes (toi_agent_group).
+// Every lane keeps the whole env in registers; the contact memory is in LDS
+// (K); agent state crosses lanes through `ag` ([AM][kAgW] of this env) at the
+// workgroup barriers, which every lane of the workgroup reaches.
+// ---------------------------------------------------------------------------
+constexpr int kAgW = 8;  // exchanged agent words: c.x c.y a v.x v.y w sleep awake
+
+template <class C, int G, class KT>
+__device__ __forceinline__ void gen_world_step(EnvL<C>& L, const Params& P, const KT& K, int I, int s, int lt,
+                                               float (*ag)[kAgW], uint32_t* woken, float dt, int64_t diag_env)
+{
+    constexpr int AM = C::AM;
+    const float inv_dt = dt > 0.0f ? 1.0f / dt : 0.0f;
+    const float dtRatio = L.inv_dt0 * dt;
+    V2 c0[AM];
+    float a0[AM];
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        c0[i] = L.c[i];
+        a0[i] = L.a[i];
+    }
+    // ---- Collide: agent-agent pairs (every lane computes; lane 0 stores) ----
+    const uint32_t at0 = K.aat();
+    uint32_t at = at0, aa_reset = 0;
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = i + 1; j < AM; ++j) {
+            if (!(bit(L.alive_m, i) && bit(L.alive_m, j))) continue;
+            if (!(bit(L.awake_m, i) || bit(L.awake_m, j))) continue;
+            const int p = aa_index<AM>(i, j);
+            const bool was = bit(at, p);
+            const V2 d = sub(L.c[j], L.c[i]);
+            const float dsq = dot(d, d);
+            const float rad = P.agent_r + P.agent_r;
+            const bool touching = !(dsq > rad * rad);
+            if (!(touching && was)) aa_reset |= 1u << p;
+            at = touching ? (at | (1u << p)) : (at & ~(1u << p));
+            if (touching != was) {
+                wake(L, i);
+                wake(L, j);
+            }
+        }
+    // ---- Collide: agent-static pair (I, s) on its lane ----
+    const int ns = kNumWalls + L.nbox;
+    const bool act = bit(L.alive_m, I) && bit(L.awake_m, I);
+    bool tch = false, ch = false;
+    const uint32_t tm = K.ast(I);
+    if (act && s < ns) {
+        const bool was = bit(tm, s);
+        const StaticG g = static_geom_dyn(L, P, s < C::NS ? s : C::NS - 1);
+        const V2 ci = sel(L.c, I);
+        const float reach = P.agent_r + kPolyRadius + 1e-3f;
+        V2 lo, hi;
+        if (s < kNumWalls) {
+            lo = mk(opq(P.wall_lo[0].x), opq(P.wall_lo[0].y));
+            hi = mk(opq(P.wall_hi[0].x), opq(P.wall_hi[0].y));
+#pragma unroll
+            for (int k = 1; k < kNumWalls; ++k)
+                if (s == k) { lo = opq(P.wall_lo[k]); hi = opq(P.wall_hi[k]); }
+        } else {
+            const int b = s - kNumWalls;
+            V2 bp = opq(L.bp[0]);
+            float hx = opq(L.bhx[0]), hy = opq(L.bhy[0]);
+#pragma unroll
+            for (int k = 1; k < C::BM; ++k)
+                if (b == k) { bp = opq(L.bp[k]); hx = opq(L.bhx[k]); hy = opq(L.bhy[k]); }
+            lo = mk(bp.x - hx, bp.y - hy);
+            hi = mk(bp.x + hx, bp.y + hy);
+        }
+        const float dx = fmaxf(fmaxf(lo.x - ci.x, ci.x - hi.x), 0.0f);
+        const float dy = fmaxf(fmaxf(lo.y - ci.y, ci.y - hi.y), 0.0f);
+        const bool cand = dx * dx + dy * dy <= reach * reach;
+        if (cand) {
+            V2 ln, lp;
+            tch = collide_pc(g.poly, g.p, g.q, ci, kPolyRadius, P.agent_r, ln, lp);
+            if (!(tch && was)) {
+                K.set_asni(I, s, 0.0f);
+                K.set_asti(I, s, 0.0f);
+            }
+        } else if (was) {
+            K.set_asni(I, s, 0.0f);
+            K.set_asti(I, s, 0.0f);
+        }
+        ch = tch != was;
+    }
+    {
+        const int lane = (int)(threadIdx.x & 63);
+        const int base = lane & ~(G - 1);
+        const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << base;
+        const uint32_t tb = (uint32_t)((__ballot(tch) & gmask) >> base);
+        const bool any_ch = (__ballot(ch) & gmask) != 0ull;
+        if (act && s == 0) {
+            K.set_ast(I, tb);
+            if (any_ch) atomicOr(woken, 1u << I);
+        }
+    }
+    __syncthreads();  // (1) agent-static updates and wakes of every group are in LDS
+    if (lt == 0) {
+        K.set_aat(at);
+#pragma unroll
+        for (int p = 0; p < C::NAA; ++p)
+            if (bit(aa_reset, p)) { K.set_aani(p, 0.0f); K.set_aati(p, 0.0f); }
+    }
+    {
+        const uint32_t wk = *woken;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+            if (bit(wk, i)) wake(L, i);
+    }
+    __syncthreads();  // (2) agent-agent memory stored; every lane read `woken`
+    if (lt == 0) *woken = 0u;
+    // ---- Solve: one island per root lane ----
+    int label[AM];
+    const uint32_t solved = island_labels(L, K, label);
+    if (s == 0 && bit(solved, I) && sel(label, I) == I) {
+        uint32_t members = 0;
+#pragma unroll
+        for (int j = 0; j < AM; ++j)
+            if (label[j] == I) members |= 1u << j;
+        StepScratch<C> S;
+        world_solve(L, P, K, S, dt, dtRatio, members & solved);
+#pragma unroll
+        for (int j = 0; j < AM; ++j) {
+            if (!bit(members & solved, j)) continue;
+            ag[j][0] = L.c[j].x; ag[j][1] = L.c[j].y; ag[j][2] = L.a[j];
+            ag[j][3] = L.v[j].x; ag[j][4] = L.v[j].y; ag[j][5] = L.w[j];
+            ag[j][6] = L.sleep[j]; ag[j][7] = bit(L.awake_m, j) ? 1.0f : 0.0f;
+        }
+    }
+    __syncthreads();  // (3) solved agents' state in LDS
+#pragma unroll
+    for (int j = 0; j < AM; ++j) {
+        if (!bit(solved, j)) continue;
+        L.c[j] = mk(ag[j][0], ag[j][1]); L.a[j] = ag[j][2];
+        L.v[j] = mk(ag[j][3], ag[j][4]); L.w[j] = ag[j][5];
+        L.sleep[j] = ag[j][6];
+        L.awake_m = ag[j][7] != 0.0f ? (L.awake_m | (1u << j)) : (L.awake_m & ~(1u << j));
+    }
+    L.inv_dt0 = inv_dt;
+    // ---- SolveTOI: agent I on its G lanes ----
+    const uint32_t toi_m = L.alive_m & L.awake_m;
+    if (bit(toi_m, I)) {
+        const uint32_t t0 = K.ast(I);
+        const ToiGroupOut o = toi_agent_group<C, G>(L, P, K, I, s, sel(c0, I), sel(a0, I), t0, dt);
+        if (s == 0) {
+            const uint32_t keep = ~((kNumWalls + L.nbox >= 32) ? 0xffffffffu : ((1u << (kNumWalls + L.nbox)) - 1u));
+            K.set_ast(I, (t0 & keep) | o.touch);
+            float* a = ag[0];
+#pragma unroll
+            for (int j = 0; j < AM; ++j)
+                if (j == I) a = ag[j];
+            a[0] = o.c.x; a[1] = o.c.y; a[2] = o.a; a[3] = o.v.x; a[4] = o.v.y; a[5] = o.w;
+            if (P.toi_diag && o.events && diag_env >= 0) atomicAdd(P.toi_diag + diag_env, o.events);
+        }
+    }
+    __syncthreads();  // (4) SolveTOI results in LDS
+#pragma unroll
+    for (int j = 0; j < AM; ++j) {
+        if (!bit(toi_m, j)) continue;
+        L.c[j] = mk(ag[j][0], ag[j][1]); L.a[j] = ag[j][2];
+        L.v[j] = mk(ag[j][3], ag[j][4]); L.w[j] = ag[j][5];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1698,8 +1883,8 @@ __device__ __forceinline__ bool world_step_fast(EnvL<C>& L, const Params& P, flo
 // own kernel, one lane per (env, agent) (k_gen_toi): TOI events of different
 // agents are independent (statics never move, agent-agent pairs are not TOI
 // pairs, and every agent SolveTOI touches is already awake).
-template <class C>
-__device__ __forceinline__ void world_step_solve(EnvL<C>& L, const Params& P, const Cont<C>& K, float dt,
+template <class C, class KT>
+__device__ __forceinline__ void world_step_solve(EnvL<C>& L, const Params& P, const KT& K, float dt,
                                                  StepScratch<C>& S)
 {
 #pragma unroll
