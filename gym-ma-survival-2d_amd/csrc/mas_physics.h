@@ -189,6 +189,16 @@ MAS_HD float pc_solve_aa(V2& cA, float& aA, V2& cB, float& aB, float r, float m,
 // TOI position iterations).
 MAS_HD float div_by_m(float x, double rm) { return (float)((double)x * rm); }
 
+// Fixed points of the Gauss-Seidel loops.  An iteration of the position or
+// velocity solver is a deterministic function of the bodies' state and the
+// accumulated impulses (the constraint data is fixed for the loop).  When an
+// iteration leaves that state bit-identical, every later iteration repeats
+// it -- same state, same separation, same exit test -- so the loop can stop
+// there with exactly the result of running all its iterations.  (The
+// reference oracle runs every iteration; parity checks the equivalence.)
+MAS_HD bool same_bits(float a, float b) { return __float_as_uint(a) == __float_as_uint(b); }
+MAS_HD bool same_bits(V2 a, V2 b) { return same_bits(a.x, b.x) && same_bits(a.y, b.y); }
+
 MAS_HD float pc_solve_as(V2 sp, Rot sq, V2 ln, V2 lp, V2& cB, float& aB, float r, float m, float I, float baum,
                          double rm)
 {
@@ -391,6 +401,18 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const K
         }
         for (int it = 0; it < 10; ++it) {
             if (!__any(sl.n > 0)) break;
+            V2 vp[AM];
+            float wp[AM], qn[C::KC], qt[C::KC];
+#pragma unroll
+            for (int i = 0; i < AM; ++i) {
+                vp[i] = L.v[i];
+                wp[i] = L.w[i];
+            }
+#pragma unroll
+            for (int q = 0; q < C::KC; ++q) {
+                qn[q] = sl.k[q].ni;
+                qt[q] = sl.k[q].ti;
+            }
 #pragma unroll
             for (int q = 0; q < C::KC; ++q) {
                 if (!__any(q < sl.n)) continue;
@@ -411,6 +433,14 @@ __device__ __forceinline__ void world_solve(EnvL<C>& L, const Params& P, const K
                     put(L.v, i, vB); put(L.w, i, wB);
                 }
             }
+            // fixed point of the whole env (see same_bits): every lane of the wave
+            bool same = true;
+#pragma unroll
+            for (int i = 0; i < AM; ++i) same = same && same_bits(L.v[i], vp[i]) && same_bits(L.w[i], wp[i]);
+#pragma unroll
+            for (int q = 0; q < C::KC; ++q)
+                if (q < sl.n) same = same && same_bits(sl.k[q].ni, qn[q]) && same_bits(sl.k[q].ti, qt[q]);
+            if (!__any(!same)) break;
         }
         // store impulses
 #pragma unroll
@@ -1475,6 +1505,8 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
 #ifdef MAS_PROFILE
                 ++npos;
 #endif
+                const V2 cp = cB;
+                const float ap = aB;
                 float minsep = 0.0f;
                 minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
 #pragma unroll
@@ -1483,6 +1515,7 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                         minsep = fmin_b2(minsep, pc_solve_as_h(sn[j], spp[j], cB, aB, r, m, Ii, kToiBaumgarte,
                                                                P.inv_mass_rcp));
                 if (minsep >= -1.5f * kLinearSlop) break;
+                if (same_bits(cB, cp) && same_bits(aB, ap)) break;  // fixed point (see same_bits)
             }
             MAS_GT(2);
             sw.c0 = cB;
@@ -1493,6 +1526,14 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
 #pragma unroll
             for (int j = 0; j < NSLOT; ++j) kq[j] = vc_init_as_h(sn[j], spp[j], ssp[j], cB, r, m, Ii);
             for (int it = 0; it < 10; ++it) {
+                const V2 vp = vB;
+                const float wp = wB, mnp = km.ni, mtp = km.ti;
+                float qn[NSLOT], qt[NSLOT];
+#pragma unroll
+                for (int j = 0; j < NSLOT; ++j) {
+                    qn[j] = kq[j].ni;
+                    qt[j] = kq[j].ti;
+                }
                 {
                     V2 vz = mk(0.0f, 0.0f);
                     float wz = 0.0f;
@@ -1505,6 +1546,11 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                     float wz = 0.0f;
                     vc_solve(kq[j], vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
                 }
+                bool same = same_bits(vB, vp) && same_bits(wB, wp) && same_bits(km.ni, mnp) && same_bits(km.ti, mtp);
+#pragma unroll
+                for (int j = 0; j < NSLOT; ++j)
+                    if (j < nsl) same = same && same_bits(kq[j].ni, qn[j]) && same_bits(kq[j].ti, qt[j]);
+                if (same) break;  // fixed point (see same_bits)
             }
         } else {
             V2 nq[C::NS], pq[C::NS];
@@ -1517,6 +1563,8 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
 #ifdef MAS_PROFILE
                 ++npos;
 #endif
+                const V2 cp = cB;
+                const float ap = aB;
                 float minsep = 0.0f;
                 minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
 #pragma unroll
@@ -1526,6 +1574,7 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                                                            P.inv_mass_rcp));
                 }
                 if (minsep >= -1.5f * kLinearSlop) break;
+                if (same_bits(cB, cp) && same_bits(aB, ap)) break;  // fixed point (see same_bits)
             }
             MAS_GT(2);
             sw.c0 = cB;
