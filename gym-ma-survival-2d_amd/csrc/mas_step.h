@@ -13,16 +13,16 @@ namespace mas {
 constexpr int kWG = 64;  // threads (= envs) per workgroup: one wave
 
 // per-thread LDS scratch
-template <class C>
+template <class C, int S = kWG>  // S: columns ([k][S] interleaved)
 struct Scr {
-    uint16_t* pairs;  // [C::AM * C::NB][kWG] (camera, agent, candidate body) of update_seen
-    uint32_t* seen;   // [C::NB][kWG] seen-by camera-position bitmask per body
-    uint8_t* perm;    // [256][kWG] spawn-grid permutation
-    int tid;
+    uint16_t* pairs;  // [C::AM * C::NB][S] (camera, agent, candidate body) of update_seen
+    uint32_t* seen;   // [C::NB][S] seen-by camera-position bitmask per body
+    uint8_t* perm;    // [256][S] spawn-grid permutation
+    int tid;          // this lane's column
     static constexpr int kPairs = C::AM * C::NB;
-    __device__ uint16_t& pr(int k) { return pairs[k * kWG + tid]; }
-    __device__ uint32_t& sn(int k) { return seen[k * kWG + tid]; }
-    __device__ uint8_t& pm(int k) { return perm[k * kWG + tid]; }
+    __device__ uint16_t& pr(int k) { return pairs[k * S + tid]; }
+    __device__ uint32_t& sn(int k) { return seen[k * S + tid]; }
+    __device__ uint8_t& pm(int k) { return perm[k * S + tid]; }
 };
 
 // unified body index in canonical (dict, then list) order
@@ -178,8 +178,8 @@ __device__ __forceinline__ void build_fixtab(const EnvL<C>& L, const Params& P, 
 // cannot intersect the segment, so its exact test would have rejected it for
 // any max fraction: the result is identical to ray_cast (the margin absorbs
 // rounding).  Loop trips = the lane's survivors, not all NB bodies.
-template <class C>
-__device__ __forceinline__ int ray_cast_tab(const EnvL<C>& L, const Params& P, const FixTab<C>& T, V2 p1, V2 p2)
+template <class C, int S>
+__device__ __forceinline__ int ray_cast_tab(const EnvL<C>& L, const Params& P, const FixTab<C, S>& T, V2 p1, V2 p2)
 {
     constexpr float m = 1e-3f;
     const V2 r = sub(p2, p1);
@@ -334,8 +334,8 @@ __device__ __forceinline__ int ray_cast_fixtab(const Params& P, const FixTab<C, 
 // vision cone and the LOS ray to pos + (1+1e-6)*d hits it first.  All
 // (camera, candidate) pairs of the env go into one list so a wave iterates
 // max(pairs per env), not sum over cameras of max(candidates per camera).
-template <class C>
-__device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, Scr<C>& scr, const FixTab<C>& T)
+template <class C, int S>
+__device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, Scr<C, S>& scr, const FixTab<C, S>& T)
 {
 #pragma unroll
     for (int k = 0; k < C::NB; ++k) scr.sn(k) = 0u;
@@ -453,8 +453,8 @@ __device__ __forceinline__ void update_seen_cam(const EnvL<C>& L, const Params& 
 }
 
 // Cameras.seen <-> state bytes (kGSeen): byte k = camera-position mask of body k
-template <class C>
-__device__ __forceinline__ void seen_pack(EnvL<C>& L, Scr<C>& scr)
+template <class C, int S>
+__device__ __forceinline__ void seen_pack(EnvL<C>& L, Scr<C, S>& scr)
 {
 #pragma unroll
     for (int w = 0; w < kSeenWords<C>; ++w) {
@@ -744,8 +744,8 @@ __device__ __forceinline__ void write_obs_row(const EnvL<C>& L, const Params& P,
 // ---------------------------------------------------------------------------
 // reset: BaseEnv.reset (masurvival_env.py:59-74) -> Simulation.reset
 // ---------------------------------------------------------------------------
-template <class C>
-__device__ __forceinline__ void env_reset(EnvL<C>& L, const Params& P, Scr<C>& scr)
+template <class C, int S>
+__device__ __forceinline__ void env_reset(EnvL<C>& L, const Params& P, Scr<C, S>& scr)
 {
     const int A = P.A, H = P.H, B = P.B;
     const int g = P.grid_size;
