@@ -22,7 +22,7 @@ using namespace mas;
 
 namespace mas {
 struct ClassInfo {
-    int words, w_rng, w_has32, w_stats, w_cont, lds_bytes;
+    int words, w_rng, w_has32, w_stats, w_cont, w_invdt, lds_bytes;
 };
 #define MAS_DECLARE(NAME)                                                                                     \
     ClassInfo class_info_##NAME();                                                                          \
@@ -299,7 +299,7 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
-    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count + [1] k_gen queue
+    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count + [1] k_gen queue + [1] last step's count
     uint8_t* gen_flag;  // [N] env left the fast path this step
     float* sweep;
     mas_obs_layout layout;
@@ -508,14 +508,15 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     }
     build_params(h);
     h->P.w_cont = h->ops.info.w_cont;
+    h->P.w_invdt = h->ops.info.w_invdt;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipMalloc(&h->state, (size_t)h->ops.info.words * (size_t)n_envs * 4);
     if (e == hipSuccess) e = hipMemset(h->state, 0, (size_t)h->ops.info.words * (size_t)n_envs * 4);
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
     h->P.prof = nullptr;
     h->phys = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 3) * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 3) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 4) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 4) * sizeof(int));
     h->sweep = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * 8 * sizeof(float));
     h->P.sweep = h->sweep;
@@ -527,6 +528,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
     h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
     h->P.gen_next = h->phys ? h->phys + n_envs + 2 : nullptr;
+    h->P.phys_last = h->phys ? h->phys + n_envs + 3 : nullptr;
     h->P.toi_diag = nullptr;
 #ifdef MAS_PROFILE
     if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
@@ -684,7 +686,7 @@ int mas_debug_counters(mas_handle* h, int64_t* host_out)
     if (!h || !host_out) return fail(MAS_ERR_INVALID_ARG, "mas_debug_counters: null argument");
     int c = 0;
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(&c, h->P.phys_count, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&c, h->P.phys_last, sizeof(int), hipMemcpyDeviceToHost));
     host_out[0] = c;
     return MAS_OK;
 }

@@ -67,6 +67,7 @@ struct Params {
     float inv_mass, inv_I, lin_damp, ang_damp;
     double inv_mass_rcp;  // 1 / (double)inv_mass (div_by_m, mas_physics.h)
     int w_cont;  // first state word of the contact memory (kGCont)
+    int w_invdt;  // state word of inv_dt0 (b2World's previous 1/dt)
     Poly4 wall_poly;
     V2 wall_pos[kNumWalls];
     float wall_angle[kNumWalls];
@@ -82,7 +83,8 @@ struct Params {
     double lid_off[kMaxLasers];
     int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
     int* phys_count;  // number of them
-    int* gen_next;    // k_gen work queue: next chunk of the list (reset by k_pre)
+    int* gen_next;    // k_gen work queue: next chunk of the list (reset by k_post)
+    int* phys_last;   // the list count of the last step (mas_debug_counters; k_post)
     uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)
     float* sweep;     // [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
     int* toi_diag;    // test diagnostics (mas_debug_set_toi_counter): per env, TOI events + 65536 per capped SolveTOI
