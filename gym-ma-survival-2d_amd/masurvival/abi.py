@@ -84,7 +84,8 @@ SIGNATURES = {
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, '_lib', 'libmas.so')
+# MAS_LIB: an alternative build of the library (A/B variants, libmas_<name>.so)
+LIB_PATH = os.environ.get('MAS_LIB') or os.path.join(PKG_DIR, '_lib', 'libmas.so')
 
 _lib = None
 
