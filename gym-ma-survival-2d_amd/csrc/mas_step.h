@@ -903,9 +903,18 @@ __device__ __forceinline__ void zone_tick(EnvL<C>& L, const Params& P)
 // pre_step hooks), step_phys (2 x world.Step + boxes Health.post_step), then
 // Cameras (update_seen) and step_post (the rest of post_step, rewards, done).
 // ---------------------------------------------------------------------------
+// the wave's melee rays, dealt over its lanes (step_pre): ray j of the wave
+// is (owner lane << 8 | agent), its segment, and its first hit
+template <class C>
+struct RayJobs {
+    uint16_t who[kWG * C::AM];
+    float x1[kWG * C::AM], y1[kWG * C::AM], x2[kWG * C::AM], y2[kWG * C::AM];
+    int16_t hit[kWG * C::AM];
+};
+
 template <class C>
 __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixTab<C>& T,
-                                         const int8_t* __restrict__ act)
+                                         const int8_t* __restrict__ act, RayJobs<C>* __restrict__ rj, bool valid)
 {
     const int A = P.A;
     // queue_actions (masurvival_env.py:741-755): alive agents only
@@ -930,18 +939,25 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
             bad = bad || x < 0 || x > hi;
             ac[i][k] = x < 0 ? 0 : (x > hi ? hi : x);
         }
-    if (bad) atomicAdd(P.bad_actions, 1);
+    if (bad && valid) atomicAdd(P.bad_actions, 1);
     // ---------------- pre_step ----------------
     // boxes: Object.pre_step drops last step's queued box items (semantics.py:853-856)
 #pragma unroll
     for (int k = 0; k < C::BM; ++k)
         if (k < L.npend) spawn_bitem(L, L.pp[k], L.phx[k], L.phy[k], L.pmeta[k]);
     L.npend = 0;
-    // agents: DynamicMotors (simulation.py:407-424)
+    // agents: DynamicMotors (simulation.py:407-424).  qs / qc: each agent's
+    // rotation, which Melee's from_polar reuses below (no module of pre_step
+    // turns a body, so it is the same rotation of the same angle)
+    float qs[C::AM], qc[C::AM];
 #pragma unroll
     for (int i = 0; i < C::AM; ++i) {
+        qs[i] = 0.0f;
+        qc[i] = 1.0f;
         if (!bit(L.alive_m, i)) continue;
         Rot q = rot_of(L.a[i]);
+        qs[i] = q.s;
+        qc[i] = q.c;
         float par = (float)(ac[i][0] - 1) * P.imp0;
         float nor = (float)(ac[i][1] - 1) * P.imp1;
         V2 J = mk(q.c * par + (-q.s) * nor, q.s * par + q.c * nor);
@@ -975,7 +991,9 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
 #pragma unroll
         for (int i = 0; i < C::AM; ++i) {
             taker[i] = -1;
-            if (!bit(L.alive_m, i)) continue;
+            // the taker query has no side effect and only a giving agent's is
+            // read (the give loop below skips the others)
+            if (!bit(L.alive_m, i) || !ac[i][5]) continue;
             V2 c = L.c[i];
             float mind = INFINITY;
             int best = -1;
@@ -1012,18 +1030,64 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
             inv_take(L, P, t, meta, hx, hy);  // full inventory: the item is lost (quirk D3)
         }
     }
-    // Melee / ContinuousMelee (semantics.py:531-554, 584-610): all rays first
+    // Melee / ContinuousMelee (semantics.py:531-554, 584-610): all rays first.
+    // A ray (laser_scan: no side effect) is cast only for an agent whose
+    // target the attack loop reads -- attacking and off cooldown; the
+    // cooldowns are those the attack loop sees (decremented after it)
     {
         int target[C::AM];
-        build_fixtab(L, P, T);
+        uint32_t need = 0;
+#pragma unroll
         for (int i = 0; i < C::AM; ++i) {
-            int tg = -1;
-            if (bit(L.alive_m, i)) {
-                V2 c = sel(L.c, i);
-                V2 hand = from_polar(P.melee_range, sel(L.a, i));
-                tg = ray_cast_tab(L, P, T, c, add(c, hand));
+            target[i] = -1;
+            const bool on_cd = P.melee_cd > 0 && L.cooldown[i] > 0;
+            if (bit(L.alive_m, i) && ac[i][3] && !on_cd) need |= 1u << i;
+        }
+        if (!valid) need = 0;  // (a lane past the last env only joins the wave's collectives)
+        // the rays of the whole wave are dealt round-robin over its 64
+        // lanes (each reads its owner env's fixture table; the same culled
+        // first-hit cast): a wave costs its mean ray count per lane, not the
+        // four rays of its busiest env (k_cameras does the same)
+        if (__any(need != 0u)) {
+            if (need) build_fixtab(L, P, T);
+            const int lane = (int)threadIdx.x & 63;
+            const int nr = __popc(need);
+            int incl = nr;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
             }
-            put(target, i, tg);
+            const int total = __shfl(incl, 63, 64);
+            const int first = incl - nr;
+            int at = first;
+#pragma unroll
+            for (int i = 0; i < C::AM; ++i) {
+                if (!bit(need, i)) continue;
+                // from_polar(range, angle) with the motors' rotation of the angle
+                const V2 c = L.c[i];
+                const V2 hand = mk(qc[i] * P.melee_range + (-qs[i]) * 0.0f, qs[i] * P.melee_range + qc[i] * 0.0f);
+                const V2 e = add(c, hand);
+                rj->who[at] = (uint16_t)((lane << 8) | i);
+                rj->x1[at] = c.x;
+                rj->y1[at] = c.y;
+                rj->x2[at] = e.x;
+                rj->y2[at] = e.y;
+                ++at;
+            }
+            __syncthreads();  // the block is this wave: the job list and the fixture tables are visible
+            for (int j = lane; j < total; j += 64) {
+                const FixTab<C> To{T.f, (int)(rj->who[j] >> 8)};
+                rj->hit[j] = (int16_t)ray_cast_fixtab(P, To, mk(rj->x1[j], rj->y1[j]), mk(rj->x2[j], rj->y2[j]));
+            }
+            __syncthreads();
+            at = first;
+#pragma unroll
+            for (int i = 0; i < C::AM; ++i) {
+                if (!bit(need, i)) continue;
+                target[i] = rj->hit[at];
+                ++at;
+            }
         }
 #pragma unroll
         for (int i = 0; i < C::AM; ++i) {
