@@ -301,6 +301,7 @@ struct mas_handle {
     uint64_t* seedbuf;
     int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count + [1] k_gen queue + [1] last step's count
     uint8_t* gen_flag;  // [N] env left the fast path this step
+    int* toi;           // [2] counts + [2][N * 8] SolveTOI (env, agent) lists (8 >= agents of every class)
     float* sweep;
     mas_obs_layout layout;
 };
@@ -529,6 +530,11 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
     h->P.gen_next = h->phys ? h->phys + n_envs + 2 : nullptr;
     h->P.phys_last = h->phys ? h->phys + n_envs + 3 : nullptr;
+    h->toi = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&h->toi, ((size_t)2 * n_envs * 8 + 2) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->toi, 0, ((size_t)2 * n_envs * 8 + 2) * sizeof(int));
+    h->P.toi_count = h->toi;
+    h->P.toi_list = h->toi ? h->toi + 2 : nullptr;
     h->P.toi_diag = nullptr;
 #ifdef MAS_PROFILE
     if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
@@ -551,6 +557,7 @@ int mas_destroy(mas_handle* h)
     if (h->P.prof) (void)hipFree(h->P.prof);
     if (h->phys) (void)hipFree(h->phys);
     if (h->sweep) (void)hipFree(h->sweep);
+    if (h->toi) (void)hipFree(h->toi);
     if (h->gen_flag) (void)hipFree(h->gen_flag);
     delete h;
     return MAS_OK;

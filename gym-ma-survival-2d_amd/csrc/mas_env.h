@@ -85,6 +85,8 @@ struct Params {
     int* phys_count;  // number of them
     int* gen_next;    // k_gen work queue: next chunk of the list (reset by k_post)
     int* phys_last;   // the list count of the last step (mas_debug_counters; k_post)
+    int* toi_list;    // [2][N * AM] (env, agent) pairs for k_gen_toi, per world step (k_gen_solve)
+    int* toi_count;   // [2] their counts (reset by k_post)
     uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)
     float* sweep;     // [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
     int* toi_diag;    // test diagnostics (mas_debug_set_toi_counter): per env, TOI events + 65536 per capped SolveTOI

@@ -376,6 +376,94 @@ __device__ __forceinline__ void update_seen(const EnvL<C>& L, const Params& P, S
     }
 }
 
+// update_seen for the reset envs of a block, with the line-of-sight rays of
+// all of them dealt over the block's lanes (one wave): each reset lane (mine)
+// lists its (camera position, camera agent, candidate body) triples -- the
+// cone test of update_seen, same order -- into `list` (at most S x AM x NB
+// 16-bit entries: column, camera position, agent, body), then every lane
+// casts list entries round-robin from the owner column's fixture table and
+// sets the body's bit in the owner's seen row with an LDS atomicOr.  Same
+// candidates, same rays, same first-hit test as update_seen; a block pays its
+// mean ray count per lane instead of one env's rays in sequence.  Every lane
+// of the block calls it (it holds two barriers).
+template <class C, int S>
+__device__ __forceinline__ void update_seen_dealt(const EnvL<C>& L, const Params& P, Scr<C, S>& scr,
+                                                  const FixTab<C, S>& T, bool mine, uint16_t* list)
+{
+    static_assert(S <= 32 && C::AM <= 8 && C::NB <= 64 && S * C::AM <= 256, "16-bit list entries");
+    constexpr int kB = C::NB <= 32 ? 5 : 6, kA = C::AM <= 2 ? 1 : (C::AM <= 4 ? 2 : 3),
+                  kC = S <= 8 ? 3 : (S <= 16 ? 4 : 5);
+    static_assert(kB + 2 * kA + kC <= 16, "16-bit list entries");
+    const int lane = (int)threadIdx.x & 63;
+    uint64_t cand[C::AM];
+    int np = 0;
+#pragma unroll
+    for (int i = 0; i < C::AM; ++i) cand[i] = 0;
+    if (mine) {
+#pragma unroll
+        for (int k = 0; k < C::NB; ++k) scr.sn(k) = 0u;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            if (!bit(L.alive_m, i)) continue;
+            const V2 pos = L.c[i];
+            const Rot q = rot_of(L.a[i]);
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b)
+                if (b < L.nbox && poly_test_point(P.cone, pos, q, L.bp[b])) cand[i] |= 1ull << (BIdx<C>::box + b);
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b)
+                if (b < L.nbi && poly_test_point(P.cone, pos, q, L.ip[b])) cand[i] |= 1ull << (BIdx<C>::bitem + b);
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h)
+                if (h < L.nheal && poly_test_point(P.cone, pos, q, L.hp[h])) cand[i] |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+            for (int w = 0; w < kNumWalls; ++w)
+                if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) cand[i] |= 1ull << (BIdx<C>::wall + w);
+#pragma unroll
+            for (int j = 0; j < C::AM; ++j)
+                if (j != i && bit(L.alive_m, j) && poly_test_point(P.cone, pos, q, L.c[j]))
+                    cand[i] |= 1ull << (BIdx<C>::agent + j);
+            np += __popcll(cand[i]);
+        }
+    }
+    int incl = np;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int total = __shfl(incl, 63, 64);
+    int at = incl - np;
+    if (mine) {
+        int p = 0;
+#pragma unroll
+        for (int i = 0; i < C::AM; ++i) {
+            if (!bit(L.alive_m, i)) continue;
+            uint64_t c = cand[i];
+            while (c) {
+                const int body = __builtin_ctzll(c);
+                c &= c - 1;
+                list[at++] = (uint16_t)((((lane << kA | p) << kA | i) << kB) | body);
+            }
+            ++p;
+        }
+    }
+    __syncthreads();  // the list and the fixture tables / zeroed seen rows are visible
+    const float eps1 = (float)(1.0 + 1e-6);
+    for (int t = lane; t < total; t += 64) {
+        const uint32_t en = list[t];
+        const int body = (int)(en & ((1u << kB) - 1)), ia = (int)((en >> kB) & ((1u << kA) - 1)),
+                  pc = (int)((en >> (kB + kA)) & ((1u << kA) - 1)), col = (int)(en >> (kB + 2 * kA));
+        const FixTab<C, S> To{T.f, col};
+        const V2 pos = mk(To.px(BIdx<C>::agent + ia), To.py(BIdx<C>::agent + ia));
+        const V2 oc = mk(To.px(body), To.py(body));
+        const V2 d = sub(oc, pos);
+        const V2 end = add(pos, scl(eps1, d));
+        if (ray_cast_fixtab(P, To, pos, end) == body) atomicOr(&scr.seen[body * S + col], 1u << pc);
+    }
+    __syncthreads();
+}
+
 // update_seen for the single camera slot `cam` (k_cameras runs one lane per
 // (env, camera) and ORs the lanes' masks).  Each lane's cone query appends
 // its (camera position, lane, body) candidates to the wave's list in LDS; the
@@ -914,9 +1002,14 @@ struct RayJobs {
 
 template <class C>
 __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixTab<C>& T,
-                                         const int8_t* __restrict__ act, RayJobs<C>* __restrict__ rj, bool valid)
+                                         const int8_t* __restrict__ act, RayJobs<C>* __restrict__ rj, bool valid,
+                                         uint32_t& dirty)
 {
     const int A = P.A;
+    // dirty: the state groups this step changed (k_pre stores only those):
+    // the agents' velocities always, the rest when a module touches them
+    dirty = kGDyn;
+    if (L.npend > 0) dirty |= kGItem | kGPend;
     // queue_actions (masurvival_env.py:741-755): alive agents only
     int ac[C::AM][6];
     // every byte load unconditional (index clamped into the env's row): the
@@ -975,6 +1068,7 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
         int meta;
         float hx, hy;
         inv_pop(L, i, meta, hx, hy);
+        dirty |= kGRule | kGStat | kGBox;
         if (it_kind(meta) == kItemHeal) {
             uses_heal++;
             agent_damage(L, P, i, P.healing, kCauseNone);
@@ -1028,6 +1122,7 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
             float hx, hy;
             inv_pop(L, i, meta, hx, hy);
             inv_take(L, P, t, meta, hx, hy);  // full inventory: the item is lost (quirk D3)
+            dirty |= kGRule;
         }
     }
     // Melee / ContinuousMelee (semantics.py:531-554, 584-610): all rays first.
@@ -1094,6 +1189,7 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
             if (!bit(L.alive_m, i)) continue;
             bool on_cd = P.melee_cd > 0 && L.cooldown[i] > 0;
             if (target[i] >= 0 && ac[i][3] && !on_cd) {
+                dirty |= kGRule | kGBox;
                 int cause = P.teams ? kCauseBadge + team_of(P, i) : i;
                 int tg = target[i];
                 if (tg >= BIdx<C>::agent) agent_damage(L, P, tg - BIdx<C>::agent, -P.melee_damage, cause);
@@ -1104,7 +1200,10 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
         if (P.melee_cd > 0) {
 #pragma unroll
             for (int i = 0; i < C::AM; ++i)
-                if (L.cooldown[i] > 0) L.cooldown[i] -= 1;
+                if (L.cooldown[i] > 0) {
+                    L.cooldown[i] -= 1;
+                    dirty |= kGRule;
+                }
         }
     }
     L.stats[17] += (float)uses_heal;
@@ -1229,9 +1328,14 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
 // K: the contact memory, touched only on deaths (k_post passes the HBM image
 // directly).  rng_used: the PCG64 stream advanced (DeathDrop draws).
 template <class C, class KT>
-__device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const KT& K, float* rew, bool& rng_used)
+__device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const KT& K, float* rew, bool& rng_used,
+                                          uint32_t& dirty)
 {
     const int A = P.A;
+    // dirty: the state groups this step changed (k_post stores only those):
+    // the zone timers and the stats always; the rest on deaths, pickups and
+    // zone damage
+    dirty = kGZone | kGStat;
     // agents: Health.post_step -> despawn dead (id order): TrackDeaths, IndexBodies,
     // DeathDrop (semantics.py:387-396), Inventory, Health.pre_despawn -> TrackKills
     uint32_t died = 0;
@@ -1243,6 +1347,7 @@ __device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const KT&
     }
     rng_used = died != 0;
     if (died) {
+        dirty |= kGDyn | kGRule | kGItem | kGHeal | kGSeen | kGRng;
         int total = 0;
 #pragma unroll
         for (int i = 0; i < C::AM; ++i)
@@ -1325,6 +1430,7 @@ __device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const KT&
                 if (inv_take(L, P, i, mk_itmeta(kItemHeal, 0, 0, kCauseNone), 0.0f, 0.0f)) takenh |= 1u << h;
             }
         }
+        if (takenb | takenh) dirty |= kGRule | kGItem | kGHeal | kGSeen;
         if (takenb) {
             int wi = 0;
 #pragma unroll
@@ -1362,7 +1468,10 @@ __device__ __forceinline__ bool step_post(EnvL<C>& L, const Params& P, const KT&
 #pragma unroll
     for (int i = 0; i < C::AM; ++i) {
         if (!bit(L.alive_m, i)) continue;
-        if (L.endgame || !circle_test_point(L.zrad, L.zpos, L.c[i])) agent_damage(L, P, i, -P.zone_damage, kCauseZone);
+        if (L.endgame || !circle_test_point(L.zrad, L.zpos, L.c[i])) {
+            agent_damage(L, P, i, -P.zone_damage, kCauseZone);
+            dirty |= kGRule;
+        }
     }
     zone_tick(L, P);
     // ---------------- compute_rewards (masurvival_env.py:757-803) ----------------
