@@ -9,7 +9,7 @@ import sys
 
 import numpy as np
 
-FAMILIES = [('general', ('k_gen<', 'k_gen_solve<', 'k_gen_toi<')), ('k_pre', ('k_pre<',)),
+FAMILIES = [('general', ('k_gen<', 'k_gen_solve<', 'k_toi_list<', 'k_gen_toi<')), ('k_pre', ('k_pre<',)),
             ('k_phys_fast', ('k_phys_fast<',)), ('k_boxes', ('k_boxes<',)), ('k_cameras', ('k_cameras<',)),
             ('k_post', ('k_post<',)), ('k_reset', ('k_reset<',)), ('k_obs', ('k_obs<',))]
 
