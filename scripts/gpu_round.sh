@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU measurement pass (run via gpurun from the repo root):
-#   scripts/gpu_round.sh <tag> [tests] [smoke] [bench] [prof] [pmc] [env]
+#   scripts/gpu_round.sh <tag> [tests] [smoke] [bench] [prof] [pmc] [env] [envprof]
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
 R=$GRAFT_REPO_ROOT
@@ -38,6 +38,11 @@ for step in "$@"; do
         -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || exit $?
       cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mas::k_" --output-format csv \
         -d $O/pmc_write -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_write.log 2>&1 || exit $? ;;
+    envprof)
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_ffa -o run -- \
+        python3 $R/bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/prof_ffa.log 2>&1 || exit $?
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_1v1 -o run -- \
+        python3 $R/bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline > $O/prof_1v1.log 2>&1 || exit $? ;;
     profgen)
       cd $R && timeout -k 10 300 python -u profiles/prof_toi.py 65536 4 > $O/prof_toi.log 2>&1 || exit $?
       cd $R && timeout -k 10 300 python -u profiles/prof_general.py 65536 20 --ppo > $O/prof_general.log 2>&1 || exit $? ;;
