@@ -507,6 +507,10 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
         delete h;
         return fail(MAS_ERR_UNSUPPORTED, "mas_create: no compiled capacity class fits this config (classes: " MAS_CLASS_LIST ")");
     }
+    if (h->ops.info.words <= 0) {
+        delete h;
+        return fail(MAS_ERR_UNSUPPORTED, "mas_create: state layout check failed (StateWords vs visit_state)");
+    }
     build_params(h);
     h->P.w_cont = h->ops.info.w_cont;
     h->P.w_invdt = h->ops.info.w_invdt;

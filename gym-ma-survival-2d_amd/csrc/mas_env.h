@@ -369,6 +369,15 @@ MAS_HD void visit_state(EnvL<C>& L, F& f, uint32_t mask = kGAll)
     f.align4();
 }
 
+// compile-time word indices of the fields the light loaders read (visit_state
+// order above; class_info checks them against it)
+template <class C>
+struct StateWords {
+    static constexpr int alive = 7 * C::AM, awake = 7 * C::AM + 1;
+    static constexpr int rule = (7 * C::AM + 2 + 3) & ~3;
+    static constexpr int box = (rule + C::AM * (4 + 3 * C::SM) + 3) & ~3;  // nbox; box b: box + 1 + 6 b ..
+};
+
 struct WordCounter {
     int n = 0;
     bool on = true;

@@ -1367,6 +1367,11 @@ struct ToiGroupOut {
 // agent's sweep start (b2Sweep c0/a0 of this world step); L: the env after
 // the island solve; K: the contact memory in HBM (impulse resets of this
 // lane's contact are written there); t0: agent I's touching word.
+// test builds: 1 sends every TOI island through the general (more contacts
+// than compact slots) branch, so the parity tests cover it
+#ifndef MAS_TOI_FORCE_FALLBACK
+#define MAS_TOI_FORCE_FALLBACK 0
+#endif
 template <class C, int G, class KT>
 __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const Params& P, const KT& K, int I, int s,
                                                        V2 c0, float a0, uint32_t t0, float dt)
@@ -1499,7 +1504,7 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
         MAS_GT(1);
         V2 cB = sw.c;
         float aB = sw.a;
-        if (nsl <= NSLOT) {
+        if (nsl <= NSLOT && !MAS_TOI_FORCE_FALLBACK) {
             // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
             for (int it = 0; it < 20; ++it) {
 #ifdef MAS_PROFILE
@@ -1553,12 +1558,13 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                 if (same) break;  // fixed point (see same_bits)
             }
         } else {
-            V2 nq[C::NS], pq[C::NS];
-#pragma unroll
-            for (int q = 0; q < C::NS; ++q) {
-                nq[q] = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
-                pq[q] = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
-            }
+            // more island contacts than compact slots (rare): every static's
+            // normal, point and position stay on its lane and are fetched by
+            // shuffle where used, and lane q keeps contact q's accumulated
+            // impulses (the group runs the serial solve in lockstep, so every
+            // lane holds the same result), so no per-static arrays live in
+            // registers for the whole kernel
+#pragma unroll 1
             for (int it = 0; it < 20; ++it) {
 #ifdef MAS_PROFILE
                 ++npos;
@@ -1567,11 +1573,12 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                 const float ap = aB;
                 float minsep = 0.0f;
                 minsep = fmin_b2(minsep, pc_solve_as_h(nm, pm, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
-#pragma unroll
+#pragma unroll 1
                 for (int q = 0; q < C::NS; ++q) {
                     if (!bit(isl, q) || q == minS) continue;
-                    minsep = fmin_b2(minsep, pc_solve_as_h(nq[q], pq[q], cB, aB, r, m, Ii, kToiBaumgarte,
-                                                           P.inv_mass_rcp));
+                    const V2 nq = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
+                    const V2 pq = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
+                    minsep = fmin_b2(minsep, pc_solve_as_h(nq, pq, cB, aB, r, m, Ii, kToiBaumgarte, P.inv_mass_rcp));
                 }
                 if (minsep >= -1.5f * kLinearSlop) break;
                 if (same_bits(cB, cp) && same_bits(aB, ap)) break;  // fixed point (see same_bits)
@@ -1580,29 +1587,30 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
             sw.c0 = cB;
             sw.a0 = aB;
             VC km = vc_init_as_h(nm, pm, sm, cB, r, m, Ii);
-            float ni[C::NS], ti[C::NS];
-#pragma unroll
-            for (int q = 0; q < C::NS; ++q) {
-                ni[q] = 0.0f;
-                ti[q] = 0.0f;
-            }
+            float ni_own = 0.0f, ti_own = 0.0f;
+#pragma unroll 1
             for (int it = 0; it < 10; ++it) {
                 {
                     V2 vz = mk(0.0f, 0.0f);
                     float wz = 0.0f;
                     vc_solve(km, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
                 }
-#pragma unroll
+#pragma unroll 1
                 for (int q = 0; q < C::NS; ++q) {
                     if (!bit(isl, q) || q == minS) continue;
-                    VC k = vc_init_as_h(nq[q], pq[q], static_pos(L, P, q), cB, r, m, Ii);
-                    k.ni = ni[q];
-                    k.ti = ti[q];
+                    const V2 nq = mk(gshfl<G>(nrm.x, q), gshfl<G>(nrm.y, q));
+                    const V2 pq = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
+                    const V2 sq = mk(gshfl<G>(g.p.x, q), gshfl<G>(g.p.y, q));
+                    VC k = vc_init_as_h(nq, pq, sq, cB, r, m, Ii);
+                    k.ni = gshfl<G>(ni_own, q);
+                    k.ti = gshfl<G>(ti_own, q);
                     V2 vz = mk(0.0f, 0.0f);
                     float wz = 0.0f;
                     vc_solve(k, vz, wz, vB, wB, 0.0f, 0.0f, m, Ii);
-                    ni[q] = k.ni;
-                    ti[q] = k.ti;
+                    if (s == q) {
+                        ni_own = k.ni;
+                        ti_own = k.ti;
+                    }
                 }
             }
         }
