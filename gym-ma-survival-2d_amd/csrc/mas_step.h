@@ -1223,39 +1223,49 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
     L.stats[18] += (float)uses_box;
 }
 
-// the agent-static rows of the contact memory (touching words and impulses)
-// in registers, for the box despawn compaction of box_health
-template <class C>
-struct ContRowsReg {
-    uint32_t t[C::AM];
-    float ni[C::AM][C::NS], ti[C::AM][C::NS];
-    template <class KT>
-    __device__ void load(const KT& K)
-    {
+// one agent's agent-static row of the contact memory (touching word and
+// impulses) shifted with the box despawn compaction of box_health: the row is
+// read once into registers, box slot k takes the row of the k-th kept box,
+// the slots past the kept boxes are cleared, and the row is written back.
+// `kept`: the boxes that stay (b < nbox, health > 0); nb: nbox before.
+template <class C, class KT>
+__device__ __forceinline__ void compact_cont_row(const KT& K, int i, uint32_t kept, int nb)
+{
+    uint32_t t = K.ast(i);
+    float ni[C::BM], ti[C::BM];
 #pragma unroll
-        for (int i = 0; i < C::AM; ++i) {
-            t[i] = K.ast(i);
-#pragma unroll
-            for (int s = 0; s < C::NS; ++s) {
-                ni[i][s] = K.asni(i, s);
-                ti[i][s] = K.asti(i, s);
-            }
-        }
+    for (int b = 0; b < C::BM; ++b) {
+        ni[b] = K.asni(i, kNumWalls + b);
+        ti[b] = K.asti(i, kNumWalls + b);
     }
-    template <class KT>
-    __device__ void store(const KT& K) const
-    {
+    int wi = 0;
 #pragma unroll
-        for (int i = 0; i < C::AM; ++i) {
-            K.set_ast(i, t[i]);
+    for (int b = 0; b < C::BM; ++b) {
+        if (b >= nb || !bit(kept, b)) continue;
 #pragma unroll
-            for (int s = 0; s < C::NS; ++s) {
-                K.set_asni(i, s, ni[i][s]);
-                K.set_asti(i, s, ti[i][s]);
-            }
+        for (int k = 0; k < C::BM; ++k) {
+            if (k != wi || k > b) continue;
+            const bool tb = bit(t, kNumWalls + b);
+            t = tb ? (t | (1u << (kNumWalls + k))) : (t & ~(1u << (kNumWalls + k)));
+            ni[k] = ni[b];
+            ti[k] = ti[b];
         }
+        ++wi;
     }
-};
+#pragma unroll
+    for (int k = 0; k < C::BM; ++k) {
+        if (k < wi) continue;
+        t &= ~(1u << (kNumWalls + k));
+        ni[k] = 0.0f;
+        ti[k] = 0.0f;
+    }
+    K.set_ast(i, t);
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        K.set_asni(i, kNumWalls + b, ni[b]);
+        K.set_asti(i, kNumWalls + b, ti[b]);
+    }
+}
 
 // boxes: Health.post_step + Object / OwnedObject despawn (semantics.py:429-435,
 // 858-861, 907-912) -- the first post_step hook (dict order: boxes group
@@ -1281,11 +1291,14 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
         }
         if (any_dead) {
             changed = true;
-            // the agent-static contact rows, read once into registers (one
-            // round trip instead of a load -> store -> load chain per word),
-            // shifted with the boxes, written back once
-            ContRowsReg<C> R;
-            R.load(K);
+            // the agent-static contact rows follow the boxes, one agent's row
+            // at a time (the rows are independent)
+            uint32_t kept = 0;
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b)
+                if (b < L.nbox && L.bhealth[b] > 0) kept |= 1u << b;
+#pragma unroll 1
+            for (int i = 0; i < C::AM; ++i) compact_cont_row<C>(K, i, kept, L.nbox);
             // stable compaction; dead boxes queue (pos, copy_shape(proto), cause)
             int wi = 0;
 #pragma unroll
@@ -1307,30 +1320,11 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
                     for (int k = 0; k < C::BM; ++k) {
                         if (k != wi || k > b) continue;
                         L.bp[k] = p; L.bhx[k] = hx; L.bhy[k] = hy; L.bmeta[k] = meta; L.bhealth[k] = hl;
-#pragma unroll
-                        for (int i = 0; i < C::AM; ++i) {
-                            const uint32_t at = R.t[i];
-                            bool tb = bit(at, kNumWalls + b);
-                            R.t[i] = tb ? (at | (1u << (kNumWalls + k))) : (at & ~(1u << (kNumWalls + k)));
-                            R.ni[i][kNumWalls + k] = R.ni[i][kNumWalls + b];
-                            R.ti[i][kNumWalls + k] = R.ti[i][kNumWalls + b];
-                        }
                     }
                     ++wi;
                 }
             }
             L.nbox = wi;
-#pragma unroll
-            for (int k = 0; k < C::BM; ++k) {
-                if (k < wi) continue;
-#pragma unroll
-                for (int i = 0; i < C::AM; ++i) {
-                    R.t[i] &= ~(1u << (kNumWalls + k));
-                    R.ni[i][kNumWalls + k] = 0.0f;
-                    R.ti[i][kNumWalls + k] = 0.0f;
-                }
-            }
-            R.store(K);
         }
     }
     return changed;
