@@ -54,6 +54,9 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
                         const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
                         float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
                         float* partials, hipStream_t s);
+int64_t policy_dw_scratch(int F, int G, int64_t K);
+hipError_t policy_dw(int F, int G, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* out,
+                     float* scratch, hipStream_t s);
 }  // namespace mas
 
 namespace {
@@ -793,6 +796,23 @@ int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const 
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_train: x must be 16-B aligned with a padded row stride");
     HIP_TRY(policy_train(packed, obs_dim, n_rows, x_bf16, x_stride, actions, old_logp, adv, ret, clip, vf_coef,
                          ent_coef, scale, h1, h2, da1, da2, dz, partials, (hipStream_t)stream));
+    return MAS_OK;
+}
+
+int64_t mas_policy_dw_scratch(int32_t f, int32_t g, int64_t k)
+{
+    return (f == 16 || f == 256) && g == 256 && k > 0 ? policy_dw_scratch(f, g, k) : -1;
+}
+
+int mas_policy_dw(int32_t f, int32_t g, int64_t k, const void* a, int64_t lda, const void* b, int64_t ldb, float* out,
+                  float* scratch, void* stream)
+{
+    const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (!(f == 16 || f == 256) || g != 256 || k <= 0 || (k % 32) != 0 || !a || !b || !out || !scratch)
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_dw: F in {16, 256}, G = 256, K a positive multiple of 32");
+    if (lda < k || ldb < k || (lda % 8) != 0 || (ldb % 8) != 0 || !al16(a) || !al16(b))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_dw: rows must be 16-B aligned (strides a multiple of 8)");
+    HIP_TRY(policy_dw(f, g, k, a, lda, b, ldb, out, scratch, (hipStream_t)stream));
     return MAS_OK;
 }
 

@@ -192,6 +192,15 @@ def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sum
     sums_out[1] = (adv.double() ** 2).sum()
 
 
+# MAS_POL_DW=1: layers 2 and 3's weight gradients through the mas_policy_dw
+# kernel instead of the split-K GEMMs.  Measured slower (r02p1, 2v2 x65536
+# minibatch of 4.2M rows): dW2 2.86 vs 1.28 ms, dW3 1.15 vs 0.52 ms -- its
+# MFMA operands come straight from global memory, 32 B per row per load
+# instruction over 256 rows 8 MB apart; an LDS-staged tile (whole 128-B lines
+# per row) is the next version.  Default off.
+_USE_DW = os.environ.get('MAS_POL_DW', '0') == '1'
+
+
 def _splitk_nt(a, b):
     """a [F, K] @ b[G, K]^T in fp32 for a huge K, as a batched GEMM over K
     chunks (bf16 in, partial sums reduced in fp32)."""
@@ -226,6 +235,7 @@ class FusedPolicy:
         assert w1.shape == (256, self.D) and w2.shape == (256, 256) and policy.head.weight.shape == (16, 256)
         self.packed = torch.empty((int(self.lib.mas_policy_packed_bytes(self.D)),), dtype=torch.uint8, device=device)
         self._bufs = None
+        self._dwbuf = {}
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -273,6 +283,19 @@ class FusedPolicy:
                           'part': torch.empty((nb, 4), dtype=torch.float32, device=self.device)}
         return self._bufs
 
+    def _dw(self, a, h, F, M):
+        """(a[:, :M] @ h[:256, :M]^T, a.sum(1)) in fp32 via mas_policy_dw."""
+        key = ('dw', F, M)
+        if key not in self._dwbuf:
+            n = int(self.lib.mas_policy_dw_scratch(F, 256, M))
+            self._dwbuf[key] = (torch.empty((n,), dtype=torch.float32, device=self.device),
+                                torch.empty((F * 256 + F,), dtype=torch.float32, device=self.device))
+        scratch, out = self._dwbuf[key]
+        check(self.lib.mas_policy_dw(F, 256, M, ctypes.c_void_p(a.data_ptr()), a.stride(0), ctypes.c_void_p(h.data_ptr()),
+                                     h.stride(0), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                                     self._stream()))
+        return out[:F * 256].view(F, 256), out[F * 256:]
+
     def grads(self, xb, actions, old_logp, adv, ret, cfg: 'PPOConfig'):
         """Sets .grad of the policy parameters to the gradient of the PPO loss
         (mean over the M rows) and returns (loss, pg, v, entropy, clipfrac)."""
@@ -288,14 +311,21 @@ class FusedPolicy:
                                         self._stream()))
         p = self.policy
         l1, l2, l3 = p.body[0], p.body[2], p.head
-        g3 = _splitk_nt(B['dz'], B['h2'])              # [16, 257]
-        g2 = _splitk_nt(B['da2'], B['h1'])             # [256, 257]
+        if _USE_DW and M % 32 == 0:
+            # layers 2 and 3: the split-K MFMA kernel (mas_policy_dw), each
+            # activation read once; layer 1 reads x row-major: a GEMM
+            g3w, g3b = self._dw(B['dz'], B['h2'], 16, M)
+            g2w, g2b = self._dw(B['da2'], B['h1'], 256, M)
+        else:
+            g3 = _splitk_nt(B['dz'], B['h2'])          # [16, 257]
+            g2 = _splitk_nt(B['da2'], B['h1'])         # [256, 257]
+            g3w, g3b, g2w, g2b = g3[:, :256], g3[:, 256], g2[:, :256], g2[:, 256]
         g1 = _splitk_nn(B['da1'], xb[:, :self.D + 1])  # [256, D + 1]
-        grads = {l3.weight: g3[:, :256], l3.bias: g3[:, 256], l2.weight: g2[:, :256], l2.bias: g2[:, 256],
+        grads = {l3.weight: g3w, l3.bias: g3b, l2.weight: g2w, l2.bias: g2b,
                  l1.weight: g1[:, :self.D], l1.bias: g1[:, self.D]}
         for prm, g in grads.items():
             if prm.grad is None:
-                prm.grad = g.to(prm.dtype).contiguous()
+                prm.grad = g.to(prm.dtype).clone(memory_format=torch.contiguous_format)
             else:
                 prm.grad.copy_(g)
         s = B['part'].sum(0) / M

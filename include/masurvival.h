@@ -233,6 +233,18 @@ int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const 
                      float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
                      float* partials, void* stream);
 
+/* mas_policy_dw: the weight and bias gradients of one policy layer from the
+ * feature-major activations mas_policy_train writes, over the minibatch rows:
+ * out[F*G + F] = (a [F][K] . b [G][K]^T, row sums of a) in fp32, a / b bf16
+ * with K contiguous (row strides lda / ldb >= K, multiples of 8, 16-B aligned
+ * rows); F = 256 (dW2 from dA2 and h1) or 16 (dW3 from dz and h2), G = 256,
+ * K a multiple of 32.  scratch: mas_policy_dw_scratch(F, G, K) floats of
+ * split-K partial sums.  Replaces the caller's GEMMs over the ones-row trick
+ * for these two layers (the dW1 GEMM reads x row-major and stays a GEMM). */
+int64_t mas_policy_dw_scratch(int32_t f, int32_t g, int64_t k);
+int mas_policy_dw(int32_t f, int32_t g, int64_t k, const void* a, int64_t lda, const void* b, int64_t ldb, float* out,
+                  float* scratch, void* stream);
+
 /* Diagnostics (synchronises the device): host_out[0] = envs of the last
  * mas_step that left the contact-free physics fast path and ran the general
  * physics kernel (contacts, TOI events, box despawns). */

@@ -9,6 +9,7 @@ value/log-prob |d| <= 0.03 + 0.03 |ref|; gradients: cosine >= 0.999 and
 relative norm error <= 3 % per parameter tensor; the bf16 input copy is
 exact."""
 import copy
+import ctypes
 
 import pytest
 
@@ -127,6 +128,36 @@ def test_policy_train_gradients_match_reference(D, M):
         ga, gb = a.grad.float(), b.grad
         assert _cos(ga, gb) >= 0.999, (name, _cos(ga, gb))
         assert float((ga.norm() - gb.norm()).abs() / gb.norm()) <= 0.03, name
+
+
+@pytest.mark.parametrize('F,K', [(256, 65536 + 32 * 37), (16, 32 * 1001), (256, 64)])
+def test_policy_dw_matches_fp32(F, K):
+    """mas_policy_dw (split-K MFMA weight + bias gradients) against torch fp32
+    on the same bf16 operands, row strides wider than K as in the trainer's
+    [257][M] activation buffers."""
+    from masurvival.abi import check, load_library
+    lib = load_library()
+    g = torch.Generator(device='cuda').manual_seed(F + K)
+    a = torch.randn((F, K + 64), device='cuda', generator=g).to(torch.bfloat16)
+    h = torch.randn((257, K + 64), device='cuda', generator=g).to(torch.bfloat16)
+    n = int(lib.mas_policy_dw_scratch(F, 256, K))
+    assert n > 0
+    scratch = torch.empty((n,), device='cuda')
+    out = torch.empty((F * 256 + F,), device='cuda')
+    check(lib.mas_policy_dw(F, 256, K, ctypes.c_void_p(a.data_ptr()), a.stride(0), ctypes.c_void_p(h.data_ptr()),
+                            h.stride(0), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()), None))
+    torch.cuda.synchronize()
+    af, hf = a[:, :K].float(), h[:256, :K].float()
+    ref_w, ref_b = af @ hf.T, af.sum(1)
+    # fp32 sums of K bf16 products in another order: |d| <= 1e-5 * sum |a||h|
+    bound_w = 1e-5 * (af.abs() @ hf.abs().T) + 1e-6
+    bound_b = 1e-5 * af.abs().sum(1) + 1e-6
+    assert bool(((out[:F * 256].view(F, 256) - ref_w).abs() <= bound_w).all())
+    assert bool(((out[F * 256:] - ref_b).abs() <= bound_b).all())
+    # bad shapes are refused
+    assert lib.mas_policy_dw(F, 256, K + 16, ctypes.c_void_p(a.data_ptr()), a.stride(0), ctypes.c_void_p(h.data_ptr()),
+                             h.stride(0), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                             None) != 0
 
 
 def test_fused_trainer_iteration_on_env():
