@@ -742,7 +742,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
 // activation byte is read from HBM once.  Measured slower than the hipBLASLt
 // split-K GEMMs it was meant to replace (dW2 2.86 vs 1.28 ms per 4.2M-row
 // minibatch): a load instruction touches 32 rows 8 MB apart for 32 B each;
-// the trainer keeps the GEMMs (ppo.py MAS_POL_DW).
+// layer 3 keeps its GEMM (ppo.py MAS_POL_DW); layer 2 runs k_dw_lds below.
 template <int WF, int WGN, int FT, int GT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_dw_nt(
     int F, int G, int64_t K, const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
@@ -846,6 +846,123 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
 }
 
+// dW = A B^T for F = G = 256 through LDS (the faster form of k_dw_nt): per
+// K-tile of kDwKT rows, both operand tiles [256][kDwKT] bf16 land in LDS by
+// LDS-DMA (global_load_lds_dwordx4; the lanes of one row read its bytes of
+// the tile contiguously), in a ring of kDwStages stages: kDwStages - 1 tiles'
+// loads are in flight while one feeds the MFMAs (each wave waits with vmcnt
+// for its oldest tile only, then a bare block barrier).  Row r's 16-B chunk c
+// sits in slot c ^ ((r / RS) % CH) of its row, so a fragment read (32 rows,
+// one chunk) is conflict-free per 16 lanes.  Thread t also sums row t of the
+// A tile (db).  Measured (4.2M-row minibatch, dW2): 64-row tiles in 2 stages
+// 1.13 ms, 32-row tiles in 4 stages 1.63 ms, the hipBLASLt GEMM 1.28 ms.
+constexpr int kDwKT = 64;                  // K rows per tile
+constexpr int kDwStages = 2;
+constexpr int kDwRowB = kDwKT * 2;         // bytes of a row in a tile
+constexpr int kDwCH = kDwKT / 8;           // 16-B chunks per row
+constexpr int kDwRS = 128 / kDwKT;         // rows per 64 banks
+constexpr int kDwRPI = 64 / kDwCH;         // rows per load instruction
+constexpr int kDwIPW = 256 / kDwRPI / 4;   // load instructions per wave per operand
+constexpr int kDwTileB = 256 * kDwRowB;    // bytes per operand tile
+__device__ __forceinline__ int dw_off(int row, int c)
+{
+    return row * kDwRowB + 16 * (c ^ ((row / kDwRS) & (kDwCH - 1)));
+}
+template <int N>
+__device__ __forceinline__ void wait_vm()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt(((N >> 4) << 14) | (N & 15) | 0xF70);  // vmcnt(N), no expcnt / lgkmcnt wait
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_dw_lds(
+    int64_t K, const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb, int64_t kc,
+    float* __restrict__ part)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDwStages][2][kDwTileB];
+    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63), r = lane & 31, h = lane >> 5;
+    const int wf = wave >> 1, wg = wave & 1;  // 128 f x 128 g per wave
+    const int64_t k0 = (int64_t)blockIdx.x * kc;
+    const int64_t k1 = k0 + kc < K ? k0 + kc : K;
+    const int nt = (int)((k1 - k0) / kDwKT);
+    const int lrow = lane / kDwCH, lslot = lane % kDwCH;
+    auto issue = [&](int t) {
+        const int st = t % kDwStages;
+        const int64_t kt = k0 + (int64_t)t * kDwKT;
+#pragma unroll
+        for (int i = 0; i < kDwIPW; ++i) {
+            const int R0 = (wave * kDwIPW + i) * kDwRPI;
+            const int row = R0 + lrow;
+            const int ch = lslot ^ ((row / kDwRS) & (kDwCH - 1));
+            __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)row * lda + kt + 8 * ch),
+                                             (lds_void*)(&lds[st][0][R0 * kDwRowB]), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)row * ldb + kt + 8 * ch),
+                                             (lds_void*)(&lds[st][1][R0 * kDwRowB]), 16, 0, 0);
+        }
+    };
+    f16v acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
+    float bsum = 0.0f;
+#pragma unroll
+    for (int t = 0; t < kDwStages - 1; ++t)
+        if (t < nt) issue(t);
+    constexpr int kPer = 2 * kDwIPW;  // this wave's load instructions per tile
+    for (int t = 0; t < nt; ++t) {
+        // this wave's loads of tile t have landed once at most the later
+        // tiles' loads are outstanding
+        const int later = nt - 1 - t < kDwStages - 2 ? nt - 1 - t : kDwStages - 2;
+        if (kDwStages > 3 && later >= 2) wait_vm<(kDwStages > 3 ? 2 * kPer : 0)>();
+        else if (kDwStages > 2 && later == 1) wait_vm<(kDwStages > 2 ? kPer : 0)>();
+        else wait_vm<0>();
+        // every wave's loads of tile t landed (each waited for its own);
+        // tile t - 1's stage is free.  A bare s_barrier: __syncthreads()'s
+        // fence would wait for the later tiles' loads too
+        __builtin_amdgcn_s_barrier();
+        if (t + kDwStages - 1 < nt) issue(t + kDwStages - 1);
+        const uint8_t* la = lds[t % kDwStages][0];
+        const uint8_t* lb = lds[t % kDwStages][1];
+#pragma unroll
+        for (int s = 0; s < kDwKT / 16; ++s) {
+            const int c = 2 * s + h;
+            bf8 a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = *(const bf8*)(la + dw_off((wf * 4 + i) * 32 + r, c));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = *(const bf8*)(lb + dw_off((wg * 4 + j) * 32 + r, c));
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+        }
+        // db: thread t sums row t of the A tile
+#pragma unroll
+        for (int c = 0; c < kDwCH; ++c) {
+            const bf8 v = *(const bf8*)(la + dw_off((int)threadIdx.x, c));
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum += (float)v[e];
+        }
+    }
+    float* rec = part + (int64_t)blockIdx.x * (256 * 256 + 256);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int g = (wg * 4 + j) * 32 + r;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int f = (wf * 4 + i) * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                rec[(int64_t)f * 256 + g] = acc[i][j][q];
+            }
+        }
+    }
+    rec[256 * 256 + threadIdx.x] = bsum;
+}
+
 // out[i] = sum over the nb partial records of part[b][i], i < n
 __global__ __launch_bounds__(256) void k_dw_reduce(int64_t n, int nb, const float* __restrict__ part,
                                                    float* __restrict__ out)
@@ -927,9 +1044,12 @@ hipError_t policy_dw(int F, int G, int64_t K, const void* A, int64_t lda, const 
 {
     const int nb = dw_blocks(K);
     int64_t kc = (K + nb - 1) / nb;
-    kc = (kc + 31) / 32 * 32;
+    kc = (kc + pol::kDwKT - 1) / pol::kDwKT * pol::kDwKT;
     const int nbu = (int)((K + kc - 1) / kc);
-    if (F == 256)
+    if (F == 256 && G == 256 && K % pol::kDwKT == 0 && kc % pol::kDwKT == 0)
+        hipLaunchKernelGGL(pol::k_dw_lds, dim3((unsigned)nbu), dim3(256), 0, s, K, (const __bf16*)A, lda,
+                           (const __bf16*)B, ldb, kc, scratch);
+    else if (F == 256)
         hipLaunchKernelGGL((pol::k_dw_nt<2, 2, 4, 4>), dim3((unsigned)nbu), dim3(256), 0, s, F, G, K,
                            (const __bf16*)A, lda, (const __bf16*)B, ldb, kc, scratch);
     else

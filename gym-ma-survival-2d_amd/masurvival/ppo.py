@@ -192,13 +192,13 @@ def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sum
     sums_out[1] = (adv.double() ** 2).sum()
 
 
-# MAS_POL_DW=1: layers 2 and 3's weight gradients through the mas_policy_dw
-# kernel instead of the split-K GEMMs.  Measured slower (r02p1, 2v2 x65536
-# minibatch of 4.2M rows): dW2 2.86 vs 1.28 ms, dW3 1.15 vs 0.52 ms -- its
-# MFMA operands come straight from global memory, 32 B per row per load
-# instruction over 256 rows 8 MB apart; an LDS-staged tile (whole 128-B lines
-# per row) is the next version.  Default off.
-_USE_DW = os.environ.get('MAS_POL_DW', '0') == '1'
+# MAS_POL_DW: the policy layers ('2', '3') whose weight gradients come from
+# the mas_policy_dw kernel instead of the split-K GEMMs (e.g. '2', '23', '0').
+# Layer 2 (F = 256) runs the LDS-staged kernel: 1.11 ms + 0.07 ms reduction
+# against 1.28 ms for its GEMM per 4.2M-row minibatch (update 30.2 -> 29.7 ms,
+# r02p4); layer 3 (F = 16) runs the direct global-operand kernel, measured
+# slower than its GEMM (1.15 vs 0.52 ms), so it stays a GEMM by default.
+_DW_LAYERS = os.environ.get('MAS_POL_DW', '2')
 
 
 def _splitk_nt(a, b):
@@ -311,15 +311,19 @@ class FusedPolicy:
                                         self._stream()))
         p = self.policy
         l1, l2, l3 = p.body[0], p.body[2], p.head
-        if _USE_DW and M % 32 == 0:
-            # layers 2 and 3: the split-K MFMA kernel (mas_policy_dw), each
-            # activation read once; layer 1 reads x row-major: a GEMM
+        # layers 2 / 3: the split-K MFMA kernel (mas_policy_dw) where enabled,
+        # else the split-K GEMM over the ones-row trick; layer 1 reads x
+        # row-major: a GEMM
+        if '3' in _DW_LAYERS and M % 32 == 0:
             g3w, g3b = self._dw(B['dz'], B['h2'], 16, M)
-            g2w, g2b = self._dw(B['da2'], B['h1'], 256, M)
         else:
             g3 = _splitk_nt(B['dz'], B['h2'])          # [16, 257]
+            g3w, g3b = g3[:, :256], g3[:, 256]
+        if '2' in _DW_LAYERS and M % 32 == 0:
+            g2w, g2b = self._dw(B['da2'], B['h1'], 256, M)
+        else:
             g2 = _splitk_nt(B['da2'], B['h1'])         # [256, 257]
-            g3w, g3b, g2w, g2b = g3[:, :256], g3[:, 256], g2[:, :256], g2[:, 256]
+            g2w, g2b = g2[:, :256], g2[:, 256]
         g1 = _splitk_nn(B['da1'], xb[:, :self.D + 1])  # [256, D + 1]
         grads = {l3.weight: g3w, l3.bias: g3b, l2.weight: g2w, l2.bias: g2b,
                  l1.weight: g1[:, :self.D], l1.bias: g1[:, self.D]}
