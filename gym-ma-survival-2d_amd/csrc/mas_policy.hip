@@ -742,7 +742,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
 // activation byte is read from HBM once.  Measured slower than the hipBLASLt
 // split-K GEMMs it was meant to replace (dW2 2.86 vs 1.28 ms per 4.2M-row
 // minibatch): a load instruction touches 32 rows 8 MB apart for 32 B each;
-// layer 3 keeps its GEMM (ppo.py MAS_POL_DW); layer 2 runs k_dw_lds below.
+// it remains for K not a multiple of 64; the trainer runs k_dw_lds below.
 template <int WF, int WGN, int FT, int GT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_dw_nt(
     int F, int G, int64_t K, const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
@@ -875,92 +875,126 @@ __device__ __forceinline__ void wait_vm()
     __builtin_amdgcn_s_waitcnt(((N >> 4) << 14) | (N & 15) | 0xF70);  // vmcnt(N), no expcnt / lgkmcnt wait
 }
 
+// FR = 256 (dW2: waves 2 x 2, 128 f x 128 g each) or 16 (dW3: the A tile's
+// rows 16..31 stay zero, waves 1 x 4, 32 f x 64 g each); ST stages.
+template <int FR, int ST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_dw_lds(
     int64_t K, const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb, int64_t kc,
     float* __restrict__ part)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDwStages][2][kDwTileB];
+    static_assert(FR == 256 || FR == 16, "F");
+    constexpr int FA = FR == 256 ? 256 : 32;  // A tile rows (16..31 zero for FR = 16)
+    constexpr int FT = FR == 256 ? 4 : 1, GT = FR == 256 ? 4 : 2;
+    constexpr int AIPW = FR == 256 ? kDwIPW : 1;  // A load instructions per loading wave
+    // one array, stage st = [A tile | B tile]: with two arrays the compiler
+    // put a vmcnt(0) before the fragment reads (the next tiles' LDS-DMA could
+    // not be told apart from them), which serialised loads and MFMAs
+    constexpr int kA = FA * kDwRowB, kStB = kA + kDwTileB;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[ST][kStB];
     const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63), r = lane & 31, h = lane >> 5;
-    const int wf = wave >> 1, wg = wave & 1;  // 128 f x 128 g per wave
+    const int wf = FR == 256 ? wave >> 1 : 0, wg = FR == 256 ? wave & 1 : wave;
     const int64_t k0 = (int64_t)blockIdx.x * kc;
     const int64_t k1 = k0 + kc < K ? k0 + kc : K;
     const int nt = (int)((k1 - k0) / kDwKT);
     const int lrow = lane / kDwCH, lslot = lane % kDwCH;
+    if (FR < FA) {
+        // the padding rows of every stage's A tile, once
+        for (int i = (int)threadIdx.x; i < ST * (FA - FR) * kDwRowB / 16; i += 256) {
+            const int st = i / ((FA - FR) * kDwRowB / 16), o = i % ((FA - FR) * kDwRowB / 16);
+            *(uint4*)(&lds[st][FR * kDwRowB + 16 * o]) = make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
+    }
     auto issue = [&](int t) {
-        const int st = t % kDwStages;
+        const int st = t % ST;
         const int64_t kt = k0 + (int64_t)t * kDwKT;
 #pragma unroll
         for (int i = 0; i < kDwIPW; ++i) {
             const int R0 = (wave * kDwIPW + i) * kDwRPI;
             const int row = R0 + lrow;
             const int ch = lslot ^ ((row / kDwRS) & (kDwCH - 1));
-            __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)row * lda + kt + 8 * ch),
-                                             (lds_void*)(&lds[st][0][R0 * kDwRowB]), 16, 0, 0);
+            if (FR == 256)  // A and B rows interleaved (measured faster than B then A)
+                __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)row * lda + kt + 8 * ch),
+                                                 (lds_void*)(&lds[st][R0 * kDwRowB]), 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)row * ldb + kt + 8 * ch),
-                                             (lds_void*)(&lds[st][1][R0 * kDwRowB]), 16, 0, 0);
+                                             (lds_void*)(&lds[st][kA + R0 * kDwRowB]), 16, 0, 0);
+        }
+        if (FR < 256 && wave * AIPW * kDwRPI < FR) {  // wave-uniform
+#pragma unroll
+            for (int i = 0; i < AIPW; ++i) {
+                const int R0 = (wave * AIPW + i) * kDwRPI;
+                const int row = R0 + lrow;
+                const int ch = lslot ^ ((row / kDwRS) & (kDwCH - 1));
+                __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)row * lda + kt + 8 * ch),
+                                                 (lds_void*)(&lds[st][R0 * kDwRowB]), 16, 0, 0);
+            }
         }
     };
-    f16v acc[4][4];
+    f16v acc[FT][GT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FT; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < GT; ++j)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.0f;
     float bsum = 0.0f;
 #pragma unroll
-    for (int t = 0; t < kDwStages - 1; ++t)
+    for (int t = 0; t < ST - 1; ++t)
         if (t < nt) issue(t);
-    constexpr int kPer = 2 * kDwIPW;  // this wave's load instructions per tile
+    // the fewest load instructions a wave issues per tile (a wave that also
+    // loads A rows waits a little longer than it must: still correct)
+    constexpr int kPer = kDwIPW + (FR == 256 ? kDwIPW : 0);
     for (int t = 0; t < nt; ++t) {
         // this wave's loads of tile t have landed once at most the later
         // tiles' loads are outstanding
-        const int later = nt - 1 - t < kDwStages - 2 ? nt - 1 - t : kDwStages - 2;
-        if (kDwStages > 3 && later >= 2) wait_vm<(kDwStages > 3 ? 2 * kPer : 0)>();
-        else if (kDwStages > 2 && later == 1) wait_vm<(kDwStages > 2 ? kPer : 0)>();
+        const int later = nt - 1 - t < ST - 2 ? nt - 1 - t : ST - 2;
+        if (ST > 3 && later >= 2) wait_vm<(ST > 3 ? 2 * kPer : 0)>();
+        else if (ST > 2 && later == 1) wait_vm<(ST > 2 ? kPer : 0)>();
         else wait_vm<0>();
         // every wave's loads of tile t landed (each waited for its own);
         // tile t - 1's stage is free.  A bare s_barrier: __syncthreads()'s
         // fence would wait for the later tiles' loads too
         __builtin_amdgcn_s_barrier();
-        if (t + kDwStages - 1 < nt) issue(t + kDwStages - 1);
-        const uint8_t* la = lds[t % kDwStages][0];
-        const uint8_t* lb = lds[t % kDwStages][1];
+        if (t + ST - 1 < nt) issue(t + ST - 1);
+        const uint8_t* la = lds[t % ST];
+        const uint8_t* lb = lds[t % ST] + kA;
 #pragma unroll
         for (int s = 0; s < kDwKT / 16; ++s) {
             const int c = 2 * s + h;
-            bf8 a[4], b[4];
+            bf8 a[FT], b[GT];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = *(const bf8*)(la + dw_off((wf * 4 + i) * 32 + r, c));
+            for (int i = 0; i < FT; ++i) a[i] = *(const bf8*)(la + dw_off((wf * FT + i) * 32 + r, c));
 #pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = *(const bf8*)(lb + dw_off((wg * 4 + j) * 32 + r, c));
+            for (int j = 0; j < GT; ++j) b[j] = *(const bf8*)(lb + dw_off((wg * GT + j) * 32 + r, c));
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < FT; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+                for (int j = 0; j < GT; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
         }
         // db: thread t sums row t of the A tile
+        if ((int)threadIdx.x < FR) {
 #pragma unroll
-        for (int c = 0; c < kDwCH; ++c) {
-            const bf8 v = *(const bf8*)(la + dw_off((int)threadIdx.x, c));
+            for (int c = 0; c < kDwCH; ++c) {
+                const bf8 v = *(const bf8*)(la + dw_off((int)threadIdx.x, c));
 #pragma unroll
-            for (int e = 0; e < 8; ++e) bsum += (float)v[e];
-        }
-    }
-    float* rec = part + (int64_t)blockIdx.x * (256 * 256 + 256);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int g = (wg * 4 + j) * 32 + r;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int f = (wf * 4 + i) * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-                rec[(int64_t)f * 256 + g] = acc[i][j][q];
+                for (int e = 0; e < 8; ++e) bsum += (float)v[e];
             }
         }
     }
-    rec[256 * 256 + threadIdx.x] = bsum;
+    float* rec = part + (int64_t)blockIdx.x * (FR * 256 + FR);
+#pragma unroll
+    for (int i = 0; i < FT; ++i) {
+#pragma unroll
+        for (int j = 0; j < GT; ++j) {
+            const int g = (wg * GT + j) * 32 + r;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int f = (wf * FT + i) * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (f < FR) rec[(int64_t)f * 256 + g] = acc[i][j][q];
+            }
+        }
+    }
+    if ((int)threadIdx.x < FR) rec[FR * 256 + threadIdx.x] = bsum;
 }
 
 // out[i] = sum over the nb partial records of part[b][i], i < n
@@ -970,6 +1004,7 @@ __global__ __launch_bounds__(256) void k_dw_reduce(int64_t n, int nb, const floa
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     float a = 0.0f;
+#pragma unroll 16
     for (int b = 0; b < nb; ++b) a += part[(int64_t)b * n + i];
     out[i] = a;
 }
@@ -1047,7 +1082,10 @@ hipError_t policy_dw(int F, int G, int64_t K, const void* A, int64_t lda, const 
     kc = (kc + pol::kDwKT - 1) / pol::kDwKT * pol::kDwKT;
     const int nbu = (int)((K + kc - 1) / kc);
     if (F == 256 && G == 256 && K % pol::kDwKT == 0 && kc % pol::kDwKT == 0)
-        hipLaunchKernelGGL(pol::k_dw_lds, dim3((unsigned)nbu), dim3(256), 0, s, K, (const __bf16*)A, lda,
+        hipLaunchKernelGGL((pol::k_dw_lds<256, pol::kDwStages>), dim3((unsigned)nbu), dim3(256), 0, s, K,
+                           (const __bf16*)A, lda, (const __bf16*)B, ldb, kc, scratch);
+    else if (F == 16 && G == 256 && K % pol::kDwKT == 0 && kc % pol::kDwKT == 0)
+        hipLaunchKernelGGL((pol::k_dw_lds<16, 4>), dim3((unsigned)nbu), dim3(256), 0, s, K, (const __bf16*)A, lda,
                            (const __bf16*)B, ldb, kc, scratch);
     else if (F == 256)
         hipLaunchKernelGGL((pol::k_dw_nt<2, 2, 4, 4>), dim3((unsigned)nbu), dim3(256), 0, s, F, G, K,

@@ -193,12 +193,11 @@ def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sum
 
 
 # MAS_POL_DW: the policy layers ('2', '3') whose weight gradients come from
-# the mas_policy_dw kernel instead of the split-K GEMMs (e.g. '2', '23', '0').
-# Layer 2 (F = 256) runs the LDS-staged kernel: 1.11 ms + 0.07 ms reduction
-# against 1.28 ms for its GEMM per 4.2M-row minibatch (update 30.2 -> 29.7 ms,
-# r02p4); layer 3 (F = 16) runs the direct global-operand kernel, measured
-# slower than its GEMM (1.15 vs 0.52 ms), so it stays a GEMM by default.
-_DW_LAYERS = os.environ.get('MAS_POL_DW', '2')
+# the mas_policy_dw kernel (LDS-staged split-K MFMA, k_dw_lds) instead of the
+# split-K GEMMs (e.g. '23', '2', '0').  Per 4.2M-row minibatch (r02p7): layer
+# 2 1.14 ms against 1.28 for its GEMM, layer 3 0.54 against 0.52 + the GEMM
+# path's split-K sum; the update 30.3 ms with '2', 29.5 with '23'.
+_DW_LAYERS = os.environ.get('MAS_POL_DW', '23')
 
 
 def _splitk_nt(a, b):

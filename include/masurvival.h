@@ -239,9 +239,9 @@ int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const 
  * with K contiguous (row strides lda / ldb >= K, multiples of 8, 16-B aligned
  * rows); F = 256 (dW2 from dA2 and h1) or 16 (dW3 from dz and h2), G = 256,
  * K a multiple of 32.  scratch: mas_policy_dw_scratch(F, G, K) floats of
- * split-K partial sums.  Replaces the caller's GEMM over the ones-row trick
- * for layer 2 (F = 256, K % 64 == 0: the LDS-staged kernel, faster than
- * hipBLASLt there); the dW1 GEMM reads x row-major and stays a GEMM. */
+ * split-K partial sums.  Replaces the caller's GEMMs over the ones-row trick
+ * for layers 2 and 3 (K % 64 == 0: the LDS-staged kernel); the dW1 GEMM
+ * reads x row-major and stays a GEMM. */
 int64_t mas_policy_dw_scratch(int32_t f, int32_t g, int64_t k);
 int mas_policy_dw(int32_t f, int32_t g, int64_t k, const void* a, int64_t lda, const void* b, int64_t ldb, float* out,
                   float* scratch, void* stream);

@@ -130,7 +130,8 @@ def test_policy_train_gradients_match_reference(D, M):
         assert float((ga.norm() - gb.norm()).abs() / gb.norm()) <= 0.03, name
 
 
-@pytest.mark.parametrize('F,K', [(256, 65536 + 64 * 37), (256, 65536 + 32 * 37), (16, 32 * 1001), (256, 64)])
+@pytest.mark.parametrize('F,K', [(256, 65536 + 64 * 37), (256, 65536 + 32 * 37), (16, 65536 + 64 * 5), (16, 32 * 1001),
+                                 (256, 64)])
 def test_policy_dw_matches_fp32(F, K):
     """mas_policy_dw (split-K MFMA weight + bias gradients) against torch fp32
     on the same bf16 operands, row strides wider than K as in the trainer's
