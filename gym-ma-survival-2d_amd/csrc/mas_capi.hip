@@ -53,7 +53,7 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
 hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, int64_t xb_stride, const int8_t* act,
                         const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
                         float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
-                        float* partials, hipStream_t s);
+                        int64_t ld, float* partials, hipStream_t s);
 int64_t policy_dw_scratch(int F, int G, int64_t K);
 hipError_t policy_dw(int F, int G, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* out,
                      float* scratch, hipStream_t s);
@@ -795,7 +795,22 @@ int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const 
     if (!policy_x_ok(obs_dim, x_stride) || (reinterpret_cast<uintptr_t>(x_bf16) & 15))
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_train: x must be 16-B aligned with a padded row stride");
     HIP_TRY(policy_train(packed, obs_dim, n_rows, x_bf16, x_stride, actions, old_logp, adv, ret, clip, vf_coef,
-                         ent_coef, scale, h1, h2, da1, da2, dz, partials, (hipStream_t)stream));
+                         ent_coef, scale, h1, h2, da1, da2, dz, n_rows, partials, (hipStream_t)stream));
+    return MAS_OK;
+}
+
+int mas_policy_train_ld(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
+                        const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
+                        float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
+                        int64_t ld, float* partials, void* stream)
+{
+    if (!packed || obs_dim <= 0 || n_rows <= 0 || !x_bf16 || !actions || !old_logp || !adv || !ret || !h1 || !h2 ||
+        !da1 || !da2 || !dz || !partials || ld < n_rows)
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_train_ld: bad argument");
+    if (!policy_x_ok(obs_dim, x_stride) || (reinterpret_cast<uintptr_t>(x_bf16) & 15))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_train_ld: x must be 16-B aligned with a padded row stride");
+    HIP_TRY(policy_train(packed, obs_dim, n_rows, x_bf16, x_stride, actions, old_logp, adv, ret, clip, vf_coef,
+                         ent_coef, scale, h1, h2, da1, da2, dz, ld, partials, (hipStream_t)stream));
     return MAS_OK;
 }
 

@@ -470,7 +470,8 @@ struct TrainArgs {
     const float* adv;       // [M] (normalised)
     const float* ret;       // [M]
     float clip, vf_coef, ent_coef, scale;  // scale = 1 / rows of the minibatch
-    __bf16 *h1, *h2, *da1, *da2, *dz;      // feature-major [256 | 16][M]
+    __bf16 *h1, *h2, *da1, *da2, *dz;      // feature-major [256 | 16][ld]
+    int64_t ld;             // their row stride (>= M; a power of two costs HBM bandwidth)
     float* partials;        // [gridDim.x][4]: sum pg, sum (v-ret)^2, sum entropy, clipped count
 };
 
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
     const bf8* F = reinterpret_cast<const bf8*>(A.packed);
     const float* FB = reinterpret_cast<const float*>(A.packed);
     const int l = threadIdx.x & 63, h = l >> 5, wv = threadIdx.x >> 6;
-    const int64_t M = A.M;
+    const int64_t M = A.M, LD = A.ld;
     const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wv) * 32;
     const int64_t row = row0 + (l & 31);
     const bool ok = row < M;
@@ -570,11 +571,11 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
         stage(wl, F + Lo.wbk(), kBk0 * 64);  // W3^T
         // feature-major activations for the weight gradients
         // wave-uniform store mode: 4 rows per lane (M % 4 == 0), 2 rows (M even), 1 row
-        const int rows_per_lane = !MAS_POL_PAIR ? 1 : (M & 3) == 0 ? MAS_POL_PAIR : (M & 1) == 0 ? 2 : 1;
+        const int rows_per_lane = !MAS_POL_PAIR ? 1 : ((M | LD) & 3) == 0 ? MAS_POL_PAIR : ((M | LD) & 1) == 0 ? 2 : 1;
         const bool pair = rows_per_lane > 1;
         auto store_rows = [&](__bf16* base, int t, const bf8 (&v)[2]) {
-            if (rows_per_lane == 4) store_rows4(base, M, row, t, h, v);
-            else store_rows2(base, M, row, t, h, v);
+            if (rows_per_lane == 4) store_rows4(base, LD, row, t, h, v);
+            else store_rows2(base, LD, row, t, h, v);
         };
         if (on && ok) {
             if (pair) {
@@ -589,8 +590,8 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int64_t f = 32 * mt + crow(i, h);
-                        A.h1[f * M + row] = h1[mt][i >> 3][i & 7];
-                        A.h2[f * M + row] = h2[mt][i >> 3][i & 7];
+                        A.h1[f * LD + row] = h1[mt][i >> 3][i & 7];
+                        A.h2[f * LD + row] = h2[mt][i >> 3][i & 7];
                     }
             }
         }
@@ -655,7 +656,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
             st[2] = ent;
             st[3] = fabsf(ratio - 1.0f) > A.clip ? 1.0f : 0.0f;
 #pragma unroll
-            for (int o = 0; o < kO; ++o) A.dz[(int64_t)o * M + row] = (__bf16)dz[o];
+            for (int o = 0; o < kO; ++o) A.dz[(int64_t)o * LD + row] = (__bf16)dz[o];
         }
         bf8 dzf[2];
 #pragma unroll
@@ -678,7 +679,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
                     store_rows(A.da2, mo, da2[mo]);
                 } else {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) A.da2[(int64_t)(32 * mo + crow(i, h)) * M + row] = da2[mo][i >> 3][i & 7];
+                    for (int i = 0; i < 16; ++i) A.da2[(int64_t)(32 * mo + crow(i, h)) * LD + row] = da2[mo][i >> 3][i & 7];
                 }
             }
         }
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
                     store_rows(A.da1, mt, d1);
                 } else {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) A.da1[(int64_t)(32 * mt + crow(i, h)) * M + row] = d1[i >> 3][i & 7];
+                    for (int i = 0; i < 16; ++i) A.da1[(int64_t)(32 * mt + crow(i, h)) * LD + row] = d1[i >> 3][i & 7];
                 }
             }
         }
@@ -1041,9 +1042,10 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
 hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, int64_t xb_stride, const int8_t* act,
                         const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
                         float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
-                        float* partials, hipStream_t s)
+                        int64_t ld, float* partials, hipStream_t s)
 {
     pol::TrainArgs A;
+    A.ld = ld;
     A.packed = (const uint8_t*)packed;
     A.ks1 = (D + 15) / 16;
     A.M = M;

@@ -79,6 +79,9 @@ SIGNATURES = {
     'mas_policy_train': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                    c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
                          + [c_void_p] * 7),
+    'mas_policy_train_ld': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+                            + [c_void_p] * 5 + [c_int64, c_void_p, c_void_p]),
     'mas_policy_dw_scratch': (c_int64, [c_int32, c_int32, c_int64]),
     'mas_policy_dw': (c_int32, [c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                 c_void_p]),

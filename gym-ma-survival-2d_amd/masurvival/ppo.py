@@ -198,16 +198,19 @@ def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sum
 # 2 1.14 ms against 1.28 for its GEMM, layer 3 0.54 against 0.52 + the GEMM
 # path's split-K sum; the update 30.3 ms with '2', 29.5 with '23'.
 _DW_LAYERS = os.environ.get('MAS_POL_DW', '23')
+# MAS_ACT_PAD: extra columns of the feature-major activation buffers (row
+# stride M + pad; 0 = the power-of-two stride: dW2 kernel 1.21 vs 0.85 ms)
+_ACT_PAD = int(os.environ.get('MAS_ACT_PAD', '64'))
 
 
 def _splitk_nt(a, b):
     """a [F, K] @ b[G, K]^T in fp32 for a huge K, as a batched GEMM over K
-    chunks (bf16 in, partial sums reduced in fp32)."""
+    chunks (bf16 in, partial sums reduced in fp32; rows may be strided)."""
     F_, K = a.shape
     G = b.shape[0]
     c = _split_k(K)
-    pa = a.view(F_, c, K // c).permute(1, 0, 2)
-    pb = b.view(G, c, K // c).permute(1, 2, 0)
+    pa = a.unflatten(1, (c, K // c)).permute(1, 0, 2)
+    pb = b.unflatten(1, (c, K // c)).permute(1, 2, 0)
     return torch.bmm(pa, pb).sum(0, dtype=torch.float32)
 
 
@@ -215,7 +218,7 @@ def _splitk_nn(a, x):
     """a [F, K] @ x [K, G] in fp32 for a huge K (x row-major, any row stride)."""
     F_, K = a.shape
     c = _split_k(K)
-    pa = a.view(F_, c, K // c).permute(1, 0, 2)
+    pa = a.unflatten(1, (c, K // c)).permute(1, 0, 2)
     px = x.reshape(c, K // c, x.shape[1]) if x.is_contiguous() else x.unflatten(0, (c, K // c))
     return torch.bmm(pa, px).sum(0, dtype=torch.float32)
 
@@ -272,13 +275,16 @@ class FusedPolicy:
         if self._bufs is None or self._bufs['M'] != M:
             bf = dict(dtype=torch.bfloat16, device=self.device)
             nb = int(self.lib.mas_policy_blocks(M))
-            # h1 / h2 carry a row of ones (row 256): dW @ [h; 1]^T yields the bias gradient as its last column
-            h1, h2 = torch.empty((257, M), **bf), torch.empty((257, M), **bf)
+            # h1 / h2 carry a row of ones (row 256): dW @ [h; 1]^T yields the bias gradient as its last column.
+            # Row stride ld = M + _ACT_PAD: a power-of-two stride (the 4.2M-row minibatch) puts every
+            # feature row on the same HBM channels (mas_policy_train_ld)
+            ld = M + _ACT_PAD
+            h1, h2 = torch.empty((257, ld), **bf), torch.empty((257, ld), **bf)
             h1[256] = 1.0
             h2[256] = 1.0
-            self._bufs = {'M': M, 'h1': h1, 'h2': h2,
-                          'da1': torch.empty((256, M), **bf), 'da2': torch.empty((256, M), **bf),
-                          'dz': torch.empty((16, M), **bf),
+            self._bufs = {'M': M, 'ld': ld, 'h1': h1, 'h2': h2,
+                          'da1': torch.empty((256, ld), **bf), 'da2': torch.empty((256, ld), **bf),
+                          'dz': torch.empty((16, ld), **bf),
                           'part': torch.empty((nb, 4), dtype=torch.float32, device=self.device)}
         return self._bufs
 
@@ -304,10 +310,11 @@ class FusedPolicy:
             assert t.is_contiguous()
         B = self._buffers(M)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        check(self.lib.mas_policy_train(ptr(self.packed), self.D, M, ptr(xb), self.Dx, ptr(actions), ptr(old_logp),
-                                        ptr(adv), ptr(ret), cfg.clip, cfg.vf_coef, cfg.ent_coef, 1.0 / M, ptr(B['h1']),
-                                        ptr(B['h2']), ptr(B['da1']), ptr(B['da2']), ptr(B['dz']), ptr(B['part']),
-                                        self._stream()))
+        check(self.lib.mas_policy_train_ld(ptr(self.packed), self.D, M, ptr(xb), self.Dx, ptr(actions),
+                                           ptr(old_logp), ptr(adv), ptr(ret), cfg.clip, cfg.vf_coef, cfg.ent_coef,
+                                           1.0 / M, ptr(B['h1']), ptr(B['h2']), ptr(B['da1']), ptr(B['da2']),
+                                           ptr(B['dz']), B['ld'], ptr(B['part']), self._stream()))
+        B = {k: (v[:, :M] if k in ('h1', 'h2', 'da1', 'da2', 'dz') else v) for k, v in B.items()}
         p = self.policy
         l1, l2, l3 = p.body[0], p.body[2], p.head
         # layers 2 / 3: the split-K MFMA kernel (mas_policy_dw) where enabled,

@@ -232,6 +232,15 @@ int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const 
                      const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
                      float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
                      float* partials, void* stream);
+/* mas_policy_train_ld: mas_policy_train with the row stride `ld` >= n_rows
+ * of h1, h2, dA1, dA2, dz ([256 | 16][ld]; mas_policy_train: ld = n_rows).
+ * A power-of-two stride (the trainer's 4.2M-row minibatch) puts every
+ * feature row on the same HBM channels; a padded one reads and writes them
+ * about 30 % faster. */
+int mas_policy_train_ld(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
+                        const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
+                        float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
+                        int64_t ld, float* partials, void* stream);
 
 /* mas_policy_dw: the weight and bias gradients of one policy layer from the
  * feature-major activations mas_policy_train writes, over the minibatch rows:
