@@ -518,8 +518,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.w_cont = h->ops.info.w_cont;
     h->P.w_invdt = h->ops.info.w_invdt;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipMalloc(&h->state, (size_t)h->ops.info.words * (size_t)n_envs * 4);
-    if (e == hipSuccess) e = hipMemset(h->state, 0, (size_t)h->ops.info.words * (size_t)n_envs * 4);
+    if (e == hipSuccess) e = hipMalloc(&h->state, (size_t)h->ops.info.words * (size_t)state_stride(n_envs) * 4);
+    if (e == hipSuccess) e = hipMemset(h->state, 0, (size_t)h->ops.info.words * (size_t)state_stride(n_envs) * 4);
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
     h->P.prof = nullptr;
     h->phys = nullptr;
@@ -662,7 +662,7 @@ int mas_render_view(mas_handle* h, int64_t env, float* out)
     return MAS_OK;
 }
 
-int64_t mas_state_bytes(const mas_handle* h) { return h ? (int64_t)h->ops.info.words * h->N * 4 : -1; }
+int64_t mas_state_bytes(const mas_handle* h) { return h ? (int64_t)h->ops.info.words * state_stride(h->N) * 4 : -1; }
 
 int mas_get_state(mas_handle* h, void* dst, void* stream)
 {

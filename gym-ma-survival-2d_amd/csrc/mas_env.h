@@ -169,13 +169,21 @@ constexpr int kLanes = 64;  // one wave per workgroup in every env kernel
 // (k_phys, k_post, k_reset): every access is by runtime pair index at LDS
 // cost instead of a select over the whole table in registers.  The HBM image
 // holds the same words in the same order (state group kGCont).
+// env stride of the state image: N + MAS_STATE_PAD envs (a padded stride
+// keeps the word rows of a power-of-two N off the same HBM channels; measured
+// no change on the latency-bound env kernels, r02q1, so 0 by default -- the
+// policy activations, which are bandwidth-bound, do pad: ppo.py _ACT_PAD)
+#ifndef MAS_STATE_PAD
+#define MAS_STATE_PAD 0
+#endif
+MAS_HD int64_t state_stride(int64_t N) { return N + MAS_STATE_PAD; }
 #ifndef MAS_STATE_VEC4
 #define MAS_STATE_VEC4 0
 #endif
 #if MAS_STATE_VEC4
-MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (((int64_t)(w >> 2)) * N + e) * 4 + (w & 3); }
+MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (((int64_t)(w >> 2)) * state_stride(N) + e) * 4 + (w & 3); }
 #else
-MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (int64_t)w * N + e; }
+MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (int64_t)w * state_stride(N) + e; }
 #endif
 
 template <class C>
