@@ -35,6 +35,23 @@ from .abi import check, load_library
 HEADS = (3, 3, 3, 2, 2, 2)
 N_LOGITS = sum(HEADS)
 
+# MAS_ROCTX=1 brackets the trainer's phases (rollout, gae, update) with roctx
+# ranges (torch.cuda.nvtx is roctx on ROCm) for rocprofv3 --marker-trace.
+_ROCTX = os.environ.get('MAS_ROCTX', '0') == '1'
+
+
+class _phase:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if _ROCTX:
+            torch.cuda.nvtx.range_push(self.name)
+
+    def __exit__(self, *exc):
+        if _ROCTX:
+            torch.cuda.nvtx.range_pop()
+
 
 @dataclass
 class PPOConfig:
@@ -553,8 +570,50 @@ class PPOTrainer:
         self._sync_rollout_policy()
         b.obs[0].copy_(b.obs[c.horizon])
 
+    # -- checkpoint / resume ------------------------------------------------
+    # The reference has no trainer (SURVEY.md §5 lists checkpointing as an
+    # auxiliary); this keeps what a resumed run needs to continue the same
+    # trajectory: fp32 master weights, Adam moments, the sampling counters and
+    # generator, the next rollout's first observation and, when the env exposes
+    # mas_get_state (VecMaSurvival), the whole batched env state.  Only tensors
+    # and plain numbers, so torch.load(weights_only=True) reads it back.
+
+    def state_dict(self):
+        sd = {'policy': self.policy.state_dict(), 'opt': self.opt.state_dict(),
+              'steps_taken': int(self.steps_taken), 'seed': int(self.seed),
+              'gen': self.gen.get_state(), 'obs0': self.buf.obs[0].detach().clone()}
+        if hasattr(self.env, 'get_state'):
+            sd['env'] = self.env.get_state().detach().clone()
+        return sd
+
+    @torch.no_grad()
+    def load_state_dict(self, sd):
+        self.policy.load_state_dict(sd['policy'])
+        self.opt.load_state_dict(sd['opt'])
+        self.steps_taken = int(sd['steps_taken'])
+        self.seed = int(sd['seed'])
+        self.gen.set_state(sd['gen'])
+        if 'env' in sd:
+            if not hasattr(self.env, 'set_state'):
+                raise ValueError('checkpoint holds an env state but this env has no set_state')
+            self.env.set_state(sd['env'].to(self.device))
+        self.buf.obs[0].copy_(sd['obs0'])
+        if self.fused is not None:
+            self.fused.pack()
+        else:
+            self._sync_rollout_policy()
+
+    def save(self, path):
+        torch.save(self.state_dict(), path)
+
+    def load(self, path):
+        self.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))
+
     def iteration(self):
-        for t in range(self.cfg.horizon):
-            self.rollout_step(t)
-        self.finish_rollout()
-        self.update()
+        with _phase('mas.rollout'):
+            for t in range(self.cfg.horizon):
+                self.rollout_step(t)
+        with _phase('mas.gae'):
+            self.finish_rollout()
+        with _phase('mas.update'):
+            self.update()

@@ -87,3 +87,32 @@ def test_sharded_rollout_matches_one_handle():
     assert torch.equal(b1.xb[:T], b2.xb[:T])
     for t_ in tr:
         t_.env.close()
+
+
+def test_checkpoint_resume_on_env(tmp_path):
+    """PPOTrainer.save after an iteration, load into a fresh trainer on a fresh
+    env: the next rollout (fused act kernel + env kernels) is bit-identical to
+    the run that never stopped -- policy, env state and sampling counters all
+    restored."""
+    n, T = 1024, 8
+    trs = []
+    env = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n), auto_reset=True)
+    tr = PPOTrainer(env, PPOConfig(horizon=T), seed=0)
+    tr.iteration()
+    path = str(tmp_path / 'ckpt.pt')
+    tr.save(path)
+    env2 = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(1000, 1000 + n), auto_reset=True)
+    tr2 = PPOTrainer(env2, PPOConfig(horizon=T), seed=5)
+    tr2.load(path)
+    for t_ in (tr, tr2):
+        for t in range(T):
+            t_.rollout_step(t)
+        trs.append(t_)
+    torch.cuda.synchronize()
+    b1, b2 = trs[0].buf, trs[1].buf
+    for name in ('obs', 'values'):
+        assert torch.equal(getattr(b1, name), getattr(b2, name)), name
+    for name in ('actions', 'logp', 'rewards', 'dones'):
+        assert torch.equal(getattr(b1, name), getattr(b2, name)), name
+    env.close()
+    env2.close()

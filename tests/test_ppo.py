@@ -130,3 +130,37 @@ def test_split_k_linear_matches_nn_linear():
     torch.testing.assert_close(x.grad, x2.grad)
     torch.testing.assert_close(a.weight.grad, b.weight.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(a.bias.grad, b.bias.grad, rtol=1e-4, atol=1e-3)
+
+
+class StatefulStandInEnv(StandInEnv):
+    """StandInEnv with VecMaSurvival's get_state/set_state (a flat uint8 buffer)."""
+
+    def get_state(self):
+        return torch.cat([self.g.get_state(), torch.tensor([self.t], dtype=torch.int64).view(torch.uint8)])
+
+    def set_state(self, buf):
+        self.g.set_state(buf[:-8].clone())
+        self.t = int(buf[-8:].clone().view(torch.int64)[0])
+
+
+def test_checkpoint_resume_continues_the_same_trajectory(tmp_path):
+    """save() after one iteration, then a fresh trainer load()s it: its next
+    iteration ends with the same parameters, Adam moments and obs as the run
+    that never stopped (policy + Adam + sampling generator + env state)."""
+    env = StatefulStandInEnv()
+    tr = _trainer(env)
+    tr.iteration()
+    path = str(tmp_path / 'ckpt.pt')
+    tr.save(path)
+    tr.iteration()
+    env2 = StatefulStandInEnv(seed=99)  # different state until the load
+    tr2 = _trainer(env2)
+    tr2.load(path)
+    tr2.iteration()
+    for a, b in zip(tr.policy.parameters(), tr2.policy.parameters()):
+        assert torch.equal(a, b)
+    s1, s2 = tr.opt.state_dict()['state'], tr2.opt.state_dict()['state']
+    for k in s1:
+        assert torch.equal(s1[k]['exp_avg'], s2[k]['exp_avg'])
+        assert torch.equal(s1[k]['exp_avg_sq'], s2[k]['exp_avg_sq'])
+    assert torch.equal(tr.buf.obs[0], tr2.buf.obs[0]) and tr.steps_taken == tr2.steps_taken
