@@ -592,7 +592,7 @@ class PPOTrainer:
         self.opt.load_state_dict(sd['opt'])
         self.steps_taken = int(sd['steps_taken'])
         self.seed = int(sd['seed'])
-        self.gen.set_state(sd['gen'])
+        self.gen.set_state(sd['gen'].cpu())  # generator states are CPU ByteTensors (map_location moves them)
         if 'env' in sd:
             if not hasattr(self.env, 'set_state'):
                 raise ValueError('checkpoint holds an env state but this env has no set_state')

@@ -24,6 +24,9 @@ for step in "$@"; do
     benchq)
       cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $?
       cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver.log 2>&1 || exit $? ;;
+    shards)
+      cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --shards 2 --no-cpu-baseline > $O/bench_driver_shards2.log 2>&1 || exit $?
+      cd $R && timeout -k 10 400 python bench.py --shards 2 --no-cpu-baseline > $O/bench_shards2.log 2>&1 || exit $? ;;
     env)
       cd $R && timeout -k 10 200 python bench.py --mode env --no-cpu-baseline > $O/bench_env.log 2>&1 || exit $?
       cd $R && timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_ffa.log 2>&1 || exit $?

@@ -110,8 +110,9 @@ def test_checkpoint_resume_on_env(tmp_path):
         trs.append(t_)
     torch.cuda.synchronize()
     b1, b2 = trs[0].buf, trs[1].buf
-    for name in ('obs', 'values'):
-        assert torch.equal(getattr(b1, name), getattr(b2, name)), name
+    # values[T] is the previous rollout's bootstrap value (finish_rollout),
+    # which only the uninterrupted trainer has computed
+    assert torch.equal(b1.obs, b2.obs) and torch.equal(b1.values[:T], b2.values[:T])
     for name in ('actions', 'logp', 'rewards', 'dones'):
         assert torch.equal(getattr(b1, name), getattr(b2, name)), name
     env.close()
