@@ -44,6 +44,12 @@ constexpr int kO = 16;    // real outputs of layer 3 (15 logits + value)
 #define MAS_POL_WAVES 4
 #endif
 constexpr int kWaves = MAS_POL_WAVES;  // waves per workgroup (4: one per SIMD, two workgroups per CU)
+// waves per workgroup of the train kernel (a value other than kWaves needs the
+// double-buffered stages, MAS_POL_DB, whose copy loop is sized by it)
+#ifndef MAS_POL_TWAVES
+#define MAS_POL_TWAVES MAS_POL_WAVES
+#endif
+constexpr int kTWaves = MAS_POL_TWAVES;
 constexpr int kLdsFrag = 4608;  // 72 KiB LDS weight stage (16-B fragments): two workgroups per CU
 constexpr int kKc = kLdsFrag / (kMT * 64);  // layer-1 k-steps per stage (9)
 constexpr int kHalf = kMT / 2 * 16 + 8;     // fragment slots of one forward half stage: W2 4 M-tiles + W3 8 k-steps
@@ -247,6 +253,84 @@ __device__ __forceinline__ void stage(bf8* __restrict__ wl, const bf8* __restric
     __syncthreads();
 }
 
+// Stagers: a call S(src, n) returns the LDS buffer holding the weights the
+// caller computes from next; every wave of the block makes the same calls.
+// Stage1: one 72-KiB buffer, copied in and drained per call (stage()).
+struct Stage1 {
+    bf8* wl;
+    __device__ __forceinline__ const bf8* operator()(const bf8* src, int n) const
+    {
+        stage(wl, src, n);
+        return wl;
+    }
+};
+
+// MAS_POL_DB (train kernel): two buffers; stage i + 1's LDS-DMA is issued
+// right after the barrier that opens stage i, so it lands while the waves
+// compute from stage i.  The stage list is the train kernel's fixed order
+// (stage_src): W1 chunks, the two forward halves, W3^T, the two W2^T halves.
+#ifndef MAS_POL_DB
+#define MAS_POL_DB 0
+#endif
+static_assert(MAS_POL_DB || kTWaves == kWaves, "a train workgroup size of its own needs MAS_POL_DB");
+constexpr int kTStagePer = kLdsFrag / (64 * kTWaves);
+__device__ __forceinline__ void stage_issue(bf8* __restrict__ wl, const bf8* __restrict__ src, int n)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < kTStagePer; ++k) {
+        const int i0 = (int)(threadIdx.x & ~63u) + k * 64 * kTWaves;
+        if (i0 < n)  // wave-uniform
+            __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane), (lds_void*)(wl + i0), 16, 0, 0);
+    }
+}
+struct Stage2 {
+    bf8* wl;  // 2 x kLdsFrag
+    const bf8* F;
+    int64_t w1, w23, wbk;
+    int ks1, nw1, i;
+    __device__ __forceinline__ const bf8* src(int j, int& n) const
+    {
+        if (j < nw1) {
+            const int k0 = j * kKc, kn = ks1 - k0 < kKc ? ks1 - k0 : kKc;
+            n = kn * kMT * 64;
+            return F + w1 + (int64_t)k0 * kMT * 64;
+        }
+        j -= nw1;
+        if (j < 2) {
+            n = kHalf * 64;
+            return F + w23 + j * kHalf * 64;
+        }
+        j -= 2;
+        if (j == 0) {
+            n = kBk0 * 64;
+            return F + wbk;
+        }
+        n = kBk1 * 64;
+        return F + wbk + (kBk0 + (j - 1) * kBk1) * 64;
+    }
+    __device__ __forceinline__ void prime()
+    {
+        int n;
+        const bf8* s0 = src(0, n);
+        __syncthreads();
+        stage_issue(wl, s0, n);
+    }
+    __device__ __forceinline__ const bf8* operator()(const bf8*, int)
+    {
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's copy of stage i landed
+        __syncthreads();                // every wave's copy landed; stage i - 1 free
+        if (i + 1 < nw1 + 5) {
+            int n;
+            const bf8* s1 = src(i + 1, n);
+            stage_issue(wl + ((i + 1) & 1) * kLdsFrag, s1, n);
+        }
+        const bf8* r = wl + (i & 1) * kLdsFrag;
+        ++i;
+        return r;
+    }
+};
+
 __device__ __forceinline__ void tanh_h1(const f16v (&acc)[kMT], const float* __restrict__ b1p, int h,
                                         bf8 (&h1)[kMT][2])
 {
@@ -263,8 +347,8 @@ __device__ __forceinline__ void tanh_h1(const f16v (&acc)[kMT], const float* __r
 // stage, 8 M-tile accumulators, then bias + tanh into the bf16 operand
 // fragments h1[mt][s].  Every wave of the block calls it (barriers); `on` =
 // the wave has rows.
-template <int KS>
-__device__ __forceinline__ void layer1_reg(bf8* __restrict__ wl, const bf8* __restrict__ W,
+template <int KS, class STG>
+__device__ __forceinline__ void layer1_reg(STG& S, const bf8* __restrict__ W,
                                            const float* __restrict__ b1p, int l, bool on, const bf8 (&x)[KS],
                                            bf8 (&h1)[kMT][2])
 {
@@ -275,7 +359,7 @@ __device__ __forceinline__ void layer1_reg(bf8* __restrict__ wl, const bf8* __re
 #pragma unroll
     for (int k0 = 0; k0 < KS; k0 += kKc) {
         const int kn = KS - k0 < kKc ? KS - k0 : kKc;
-        stage(wl, W + k0 * kMT * 64, kn * kMT * 64);
+        const bf8* wl = S(W + k0 * kMT * 64, kn * kMT * 64);
         if (on) {
 #pragma unroll
             for (int ks = k0; ks < k0 + kn; ++ks) {
@@ -290,8 +374,8 @@ __device__ __forceinline__ void layer1_reg(bf8* __restrict__ wl, const bf8* __re
 
 // layer 1 for any obs_dim: W1 staged through LDS in chunks of kKc k-steps, x
 // fragments loaded per k-step by xf(ks)
-template <class XF>
-__device__ __forceinline__ void layer1(bf8* __restrict__ wl, const bf8* __restrict__ W, const float* __restrict__ b1p,
+template <class XF, class STG>
+__device__ __forceinline__ void layer1(STG& S, const bf8* __restrict__ W, const float* __restrict__ b1p,
                                        int ks1, int l, bool on, XF xf, bf8 (&h1)[kMT][2])
 {
     f16v acc[kMT];
@@ -299,7 +383,7 @@ __device__ __forceinline__ void layer1(bf8* __restrict__ wl, const bf8* __restri
     for (int mt = 0; mt < kMT; ++mt) acc[mt] = f16v{};
     for (int k0 = 0; k0 < ks1; k0 += kKc) {
         const int kn = ks1 - k0 < kKc ? ks1 - k0 : kKc;
-        stage(wl, W + (int64_t)k0 * kMT * 64, kn * kMT * 64);
+        const bf8* wl = S(W + (int64_t)k0 * kMT * 64, kn * kMT * 64);
         if (on) {
 #pragma unroll 2
             for (int ks = 0; ks < kn; ++ks) {
@@ -315,8 +399,8 @@ __device__ __forceinline__ void layer1(bf8* __restrict__ wl, const bf8* __restri
 
 // layer 2 (by output M-tile) fused with layer 3, in two LDS half stages;
 // h2 kept when KEEP.  Every wave of the block calls it (barriers).
-template <bool KEEP>
-__device__ __forceinline__ f16v layers23(bf8* __restrict__ wl, const bf8* __restrict__ W23,
+template <bool KEEP, class STG>
+__device__ __forceinline__ f16v layers23(STG& S, const bf8* __restrict__ W23,
                                          const float* __restrict__ b2p, int l, bool on, const bf8 (&h1)[kMT][2],
                                          bf8 (&h2)[kMT][2])
 {
@@ -324,7 +408,7 @@ __device__ __forceinline__ f16v layers23(bf8* __restrict__ wl, const bf8* __rest
     f16v z3 = f16v{};
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-        stage(wl, W23 + hf * kHalf * 64, kHalf * 64);
+        const bf8* wl = S(W23 + hf * kHalf * 64, kHalf * 64);
         if (!on) continue;
 #pragma unroll
         for (int q = 0; q < kMT / 2; ++q) {
@@ -373,6 +457,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
                                                              float* __restrict__ value)
 {
     __shared__ bf8 wl[kLdsFrag];
+    Stage1 S{wl};
     const Layout Lo{ks1};
     const bf8* F = reinterpret_cast<const bf8*>(packed);
     const float* FB = reinterpret_cast<const float*>(packed);
@@ -396,9 +481,9 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x[ks];
         }
-        layer1_reg<KS>(wl, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
+        layer1_reg<KS>(S, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
     } else {
-        layer1(wl, F + Lo.w1(), FB + Lo.b1(), ks1, l, on,
+        layer1(S, F + Lo.w1(), FB + Lo.b1(), ks1, l, on,
                [&](int ks) {
                    const bf8 x = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
                    if (xb != nullptr && ok) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x;
@@ -406,7 +491,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
                },
                h1);
     }
-    const f16v z3 = layers23<false>(wl, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);  // last barrier
+    const f16v z3 = layers23<false>(S, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);  // last barrier
     if (!on) return;
     if (h != 0 || !ok) return;
     if (MAS_POL_EXP & 2) {
@@ -541,15 +626,22 @@ __device__ __forceinline__ void store_rows4(__bf16* base, int64_t M, int64_t row
 }
 
 template <int KS>
-__global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_policy_train(TrainArgs A)
+__global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_policy_train(TrainArgs A)
 {
-    __shared__ bf8 wl[kLdsFrag];
     const Layout Lo{A.ks1};
     const bf8* F = reinterpret_cast<const bf8*>(A.packed);
     const float* FB = reinterpret_cast<const float*>(A.packed);
+#if MAS_POL_DB
+    __shared__ bf8 wl[2 * kLdsFrag];
+    Stage2 S{wl, F, Lo.w1(), Lo.w23(), Lo.wbk(), A.ks1, (A.ks1 + kKc - 1) / kKc, 0};
+    S.prime();
+#else
+    __shared__ bf8 wl[kLdsFrag];
+    Stage1 S{wl};
+#endif
     const int l = threadIdx.x & 63, h = l >> 5, wv = threadIdx.x >> 6;
     const int64_t M = A.M, LD = A.ld;
-    const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wv) * 32;
+    const int64_t row0 = ((int64_t)blockIdx.x * kTWaves + wv) * 32;
     const int64_t row = row0 + (l & 31);
     const bool ok = row < M;
     float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -563,12 +655,12 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
             bf8 x[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) x[ks] = xf(ks);
-            layer1_reg<KS>(wl, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
+            layer1_reg<KS>(S, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
         } else {
-            layer1(wl, F + Lo.w1(), FB + Lo.b1(), A.ks1, l, on, xf, h1);
+            layer1(S, F + Lo.w1(), FB + Lo.b1(), A.ks1, l, on, xf, h1);
         }
-        const f16v z3 = layers23<true>(wl, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);
-        stage(wl, F + Lo.wbk(), kBk0 * 64);  // W3^T
+        const f16v z3 = layers23<true>(S, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);
+        const bf8* wb = S(F + Lo.wbk(), kBk0 * 64);  // W3^T
         // feature-major activations for the weight gradients
         // wave-uniform store mode: 4 rows per lane (M % 4 == 0), 2 rows (M even), 1 row
         const int rows_per_lane = !MAS_POL_PAIR ? 1 : ((M | LD) & 3) == 0 ? MAS_POL_PAIR : ((M | LD) & 1) == 0 ? 2 : 1;
@@ -663,7 +755,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
         for (int i = 0; i < 16; ++i) dzf[i >> 3][i & 7] = (__bf16)dz[i];
         // dA2 = (W3^T dz) * (1 - h2^2), by M-tile of layer 2
         bf8 da2[kMT][2];
-        const bf8* W3T = wl + l;
+        const bf8* W3T = wb + l;
 #pragma unroll
         for (int mo = 0; mo < kMT; ++mo) {
             f16v g = f16v{};
@@ -684,11 +776,11 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
             }
         }
         // dA1 = (W2^T dA2) * (1 - h1^2), by M-tile of layer 1
-        const bf8* W2T = wl + l;
+        const bf8* W2T = wb + l;
 #pragma unroll
         for (int mt = 0; mt < kMT; ++mt) {
             if (mt % (kMT / 2) == 0)  // W2^T M-tiles 0..3, then 4..7
-                stage(wl, F + Lo.wbk() + (kBk0 + (mt / (kMT / 2)) * kBk1) * 64, kBk1 * 64);
+                W2T = S(F + Lo.wbk() + (kBk0 + (mt / (kMT / 2)) * kBk1) * 64, kBk1 * 64) + l;
             f16v g = f16v{};
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk) g = mfma(W2T[((mt % (kMT / 2)) * 16 + kk) * 64], da2[kk >> 1][kk & 1], g);
@@ -722,7 +814,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC * 4 / kWaves) void k_polic
     if (threadIdx.x < 4) {
         float v = 0.0f;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) v += red[w * 4 + threadIdx.x];
+        for (int w = 0; w < kTWaves; ++w) v += red[w * 4 + threadIdx.x];
         A.partials[(int64_t)blockIdx.x * 4 + threadIdx.x] = v;
     }
 }
@@ -1026,7 +1118,9 @@ hipError_t policy_pack(int D, const float* W1, const float* b1, const float* W2,
     return hipGetLastError();
 }
 
-int64_t policy_blocks(int64_t M) { return (M + 32 * pol::kWaves - 1) / (32 * pol::kWaves); }
+// workgroups of the train kernel (= its partial records) and of the act kernel
+int64_t policy_blocks(int64_t M) { return (M + 32 * pol::kTWaves - 1) / (32 * pol::kTWaves); }
+static int64_t act_blocks(int64_t M) { return (M + 32 * pol::kWaves - 1) / (32 * pol::kWaves); }
 
 hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, void* xb, int64_t xb_stride,
                       uint64_t seed, uint64_t step, int64_t first_row, int8_t* act, float* logp, float* value,
@@ -1034,7 +1128,7 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
 {
     const int ks1 = (D + 15) / 16;
     auto k = ks1 == 10 ? pol::k_policy_act<10> : ks1 == 9 ? pol::k_policy_act<9> : pol::k_policy_act<0>;
-    hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
+    hipLaunchKernelGGL(k, dim3((unsigned)act_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
                        ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, first_row, act, logp, value);
     return hipGetLastError();
 }
@@ -1066,7 +1160,7 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     A.dz = (__bf16*)dz;
     A.partials = partials;
     auto k = A.ks1 == 10 ? pol::k_policy_train<10> : A.ks1 == 9 ? pol::k_policy_train<9> : pol::k_policy_train<0>;
-    hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kWaves), 0, s, A);
+    hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kTWaves), 0, s, A);
     return hipGetLastError();
 }
 
