@@ -574,11 +574,21 @@ struct TrainArgs {
 #ifndef MAS_POL_OCC
 #define MAS_POL_OCC 2
 #endif
+// feature-major activation buffers of at most 2^32 bytes (257 rows of ld
+// bf16): the store offsets fit in 32 bits
+constexpr int64_t kOff32Ld = ((int64_t)1 << 32) / (2 * 257);
+template <bool OFF32>
 __device__ __forceinline__ void store_rows2(__bf16* base, int64_t M, int64_t row, int mt, int h, const bf8 (&v)[2])
 {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const bool odd = row & 1;
+    // feature crow(2j + odd, h) = K(j) + odd + 4 h with K(j) = 2 (j & 1) + 8 (j >> 1).
+    // OFF32: the lane's byte offset (feature odd + 4 h, column row & ~1) plus
+    // the wave-uniform K rows of M (a scalar multiply), from the buffer base:
+    // one vector add per store instead of a 64-bit multiply-add
     uint32_t* dst = reinterpret_cast<uint32_t*>(base + (row & ~(int64_t)1));
+    const uint32_t m2 = OFF32 ? __builtin_amdgcn_readfirstlane((uint32_t)(M * 2)) : 0u;
+    const uint32_t lane_off = OFF32 ? ((uint32_t)((int)odd + 4 * h) * m2 + (uint32_t)(row & ~(int64_t)1) * 2u) : 0u;
     const u4 w[2] = {__builtin_bit_cast(u4, v[0]), __builtin_bit_cast(u4, v[1])};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -587,8 +597,13 @@ __device__ __forceinline__ void store_rows2(__bf16* base, int64_t M, int64_t row
         // quad_perm [1, 0, 3, 2]: lane l reads lane l ^ 1
         const uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? a : b), 0xB1, 0xF, 0xF, false) & 0xffffu;
         const uint32_t word = odd ? (r | (b << 16)) : (a | (r << 16));
-        const int64_t f = 32 * mt + crow(odd ? 2 * j + 1 : 2 * j, h);
-        dst[(f * M) >> 1] = word;
+        if (OFF32) {
+            const uint32_t K = (uint32_t)(32 * mt + 2 * (j & 1) + 8 * (j >> 1));
+            *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(base) + (lane_off + K * m2)) = word;
+        } else {
+            const int64_t f = 32 * mt + crow(odd ? 2 * j + 1 : 2 * j, h);
+            dst[(f * M) >> 1] = word;
+        }
     }
 }
 
@@ -625,7 +640,7 @@ __device__ __forceinline__ void store_rows4(__bf16* base, int64_t M, int64_t row
     }
 }
 
-template <int KS>
+template <int KS, bool OFF32>
 __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_policy_train(TrainArgs A)
 {
     const Layout Lo{A.ks1};
@@ -667,7 +682,7 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
         const bool pair = rows_per_lane > 1;
         auto store_rows = [&](__bf16* base, int t, const bf8 (&v)[2]) {
             if (rows_per_lane == 4) store_rows4(base, LD, row, t, h, v);
-            else store_rows2(base, LD, row, t, h, v);
+            else store_rows2<OFF32>(base, LD, row, t, h, v);
         };
         if (on && ok) {
             if (pair) {
@@ -1159,7 +1174,10 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     A.da2 = (__bf16*)da2;
     A.dz = (__bf16*)dz;
     A.partials = partials;
-    auto k = A.ks1 == 10 ? pol::k_policy_train<10> : A.ks1 == 9 ? pol::k_policy_train<9> : pol::k_policy_train<0>;
+    const bool o32 = ld <= pol::kOff32Ld;
+    auto k = A.ks1 == 10 ? (o32 ? pol::k_policy_train<10, true> : pol::k_policy_train<10, false>)
+             : A.ks1 == 9 ? (o32 ? pol::k_policy_train<9, true> : pol::k_policy_train<9, false>)
+                          : (o32 ? pol::k_policy_train<0, true> : pol::k_policy_train<0, false>);
     hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kTWaves), 0, s, A);
     return hipGetLastError();
 }
