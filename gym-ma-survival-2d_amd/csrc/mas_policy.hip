@@ -242,12 +242,16 @@ typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ void stage(bf8* __restrict__ wl, const bf8* __restrict__ src, int n)
 {
     __syncthreads();  // every wave is done with the previous stage
-    const int lane = threadIdx.x & 63;
+    // the wave's first fragment in a scalar register and the lane's byte
+    // offset in a 32-bit one: each copy is a uniform base + that offset
+    const int w0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+    const uint32_t loff = (threadIdx.x & 63) * 16u;
 #pragma unroll
     for (int k = 0; k < kStagePer; ++k) {
-        const int i0 = (int)(threadIdx.x & ~63u) + k * 64 * kWaves;  // the wave's first fragment
+        const int i0 = w0 + k * 64 * kWaves;  // the wave's first fragment
         if (i0 < n)  // wave-uniform
-            __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane), (lds_void*)(wl + i0), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint8_t*>(src + i0) + loff),
+                                             (lds_void*)(wl + i0), 16, 0, 0);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -276,12 +280,14 @@ static_assert(MAS_POL_DB || kTWaves == kWaves, "a train workgroup size of its ow
 constexpr int kTStagePer = kLdsFrag / (64 * kTWaves);
 __device__ __forceinline__ void stage_issue(bf8* __restrict__ wl, const bf8* __restrict__ src, int n)
 {
-    const int lane = threadIdx.x & 63;
+    const int w0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+    const uint32_t loff = (threadIdx.x & 63) * 16u;
 #pragma unroll
     for (int k = 0; k < kTStagePer; ++k) {
-        const int i0 = (int)(threadIdx.x & ~63u) + k * 64 * kTWaves;
+        const int i0 = w0 + k * 64 * kTWaves;
         if (i0 < n)  // wave-uniform
-            __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane), (lds_void*)(wl + i0), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint8_t*>(src + i0) + loff),
+                                             (lds_void*)(wl + i0), 16, 0, 0);
     }
 }
 struct Stage2 {

@@ -2,7 +2,8 @@
 # policy train kernel with 32-bit store offsets: GPU tests, policy micro-bench,
 # driver-shaped bench; every step under its own time limit
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/off32
+TAG=${1:-off32}
+O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { echo "tests failed"; exit 1; }
