@@ -64,23 +64,32 @@ def cpu_info():
     return model, avail
 
 
-def cpu_baseline(config, leg_s=6.0):
+def cpu_baseline(config, leg_s=6.0, all_cores=False):
     """The C oracle (scalar restatement, oracle/ora_bench.c: the whole loop in
     C, no per-step ctypes call) on bounded samples, SURVEY.md 8(d):
       (i)   1v1 (C1), 1 env, 1 thread;
       (ii)  the bench config, 64 envs round-robin, 1 thread;
       (iii) the bench config, T threads (T = min(16, CPUs this process may use:
-            the GPU box's per-GPU CPU share is 16)), 64 envs per thread.
+            the GPU box's per-GPU CPU share is 16)), 64 envs per thread;
+      (iv)  the bench config on every CPU this process may use
+            (len(os.sched_getaffinity(0))), 64 envs per
+            thread -- only with all_cores (bench.py --cpu-all-cores): the
+            GPU box's host is shared by the jobs of its 8 GPUs and each job's
+            share is 16 CPUs, so the default run reports leg (iii) scaled
+            linearly to all CPUs instead, labelled as an extrapolation.
     Uniform-random actions, auto-reset.  `value` is leg (iii)."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle
     from masurvival.config import NAMED_CONFIGS, ResolvedConfig, pcg64_state
     model, avail = cpu_info()
     threads = max(1, min(16, avail))
+    runs = [('c1_1env_1thread', '1v1', 1, 1),
+            (f'{config}_64envs_1thread', config, 64, 1),
+            (f'{config}_{64 * threads}envs_{threads}threads', config, 64 * threads, threads)]
+    if all_cores and avail > threads:
+        runs.append((f'{config}_{64 * avail}envs_{avail}threads_all_cores', config, 64 * avail, avail))
     legs = []
-    for name, cfg_name, n, th in [('c1_1env_1thread', '1v1', 1, 1),
-                                  (f'{config}_64envs_1thread', config, 64, 1),
-                                  (f'{config}_{64 * threads}envs_{threads}threads', config, 64 * threads, threads)]:
+    for name, cfg_name, n, th in runs:
         rc = ResolvedConfig(NAMED_CONFIGS[cfg_name])
         st = np.stack([pcg64_state(s) for s in range(n)])
         steps, secs = oracle.bench_run(rc.to_struct(), st, th, leg_s)
@@ -91,6 +100,10 @@ def cpu_baseline(config, leg_s=6.0):
            'sample': f'C oracle (oracle/ora_bench.c), {config}, {64 * threads} envs on {threads} threads, '
                      f'random actions + auto-reset, {legs[2]["seconds"]:.1f} s; other legs listed',
            'cpu_model': model, 'cpus_available': avail, 'legs': legs}
+    if len(legs) == 3:
+        out['all_cores_extrapolated'] = {
+            'cpus': avail, 'agent_env_steps_per_s': legs[2]['agent_env_steps_per_s'] * avail / threads,
+            'what': f'leg {legs[2]["leg"]} x {avail}/{threads} (linear; measure with bench.py --cpu-all-cores)'}
     proxy = os.path.join(ROOT, 'profiles', 'r02_reference_proxy.json')
     if os.path.exists(proxy):
         p = json.load(open(proxy))
@@ -141,6 +154,8 @@ def parse_args():
                     help='ppo: policy forward + env step + buffer, GAE + PPO update every horizon; env: random actions')
     ap.add_argument('--horizon', type=int, default=64)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-all-cores', action='store_true',
+                    help='add the CPU-baseline leg on every CPU this process may use (cpu_baseline leg iv)')
     ap.add_argument('--lib', default=None, help='alternative libmas*.so (A/B variants)')
     ap.add_argument('--shards', type=int, default=1,
                     help='env handles per GPU, each on its own HIP stream (vec_env.ShardedVecMaSurvival)')
@@ -361,7 +376,7 @@ def main():
             line['roofline']['traffic_source'] = f'profiles/{tname} (FETCH_SIZE+WRITE_SIZE per mas_step)'
             break
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(args.config)
+        line['cpu_baseline'] = cpu_baseline(args.config, all_cores=args.cpu_all_cores)
     if rank == 0:
         print(json.dumps(line), flush=True)
     env.close()

@@ -70,6 +70,10 @@ class PPOConfig:
     # fused HIP policy kernels (mas_policy_act / mas_policy_train): default on
     # a GPU when hidden == 256; the torch path stays as the CPU / reference path
     fused: Optional[bool] = None
+    # the advantage-statistics and gradient all-reduces: None = when the
+    # process group has more than one rank; True forces them at world size 1
+    # too (the one-GPU RCCL test runs the exact calls of the 8-GPU bench)
+    allreduce: Optional[bool] = None
 
 
 def _split_k(m: int, cap: int = int(os.environ.get('MAS_SPLITK_CAP', '64'))) -> int:
@@ -418,6 +422,9 @@ class PPOTrainer:
         self.device = env.device
         self.group = group
         self.world = dist.get_world_size(group) if group is not None or dist.is_initialized() else 1
+        self.collectives = self.world > 1 if cfg.allreduce is None else bool(cfg.allreduce)
+        if self.collectives and not (group is not None or dist.is_initialized()):
+            raise ValueError('PPOConfig.allreduce=True needs an initialised torch.distributed process group')
         torch.manual_seed(seed)  # identical init on every rank
         self.policy = PolicyMLP(env.obs_dim, cfg.hidden).to(self.device)
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr, eps=1e-5)
@@ -511,7 +518,7 @@ class PPOTrainer:
         self.gae_impl(b.rewards, b.values, b.dones, c.gamma, c.lam, b.adv, b.ret, b.adv_sums, self.env.n_agents)
         stats = torch.cat([b.adv_sums, torch.tensor([float(b.adv.numel())], device=self.device,
                                                      dtype=torch.float64)])
-        if self.world > 1:
+        if self.collectives:
             dist.all_reduce(stats, group=self.group)
         mean = stats[0] / stats[2]
         var = (stats[1] / stats[2] - mean * mean).clamp_min(0.0)
@@ -530,7 +537,7 @@ class PPOTrainer:
                 M = xb.shape[0]
                 loss, pg, vl, ent, cf = self.fused.grads(xb, b.actions[sl].reshape(M, 6), b.logp[sl].reshape(M),
                                                          b.adv[sl].reshape(M), b.ret[sl].reshape(M), c)
-                if self.world > 1:
+                if self.collectives:
                     _allreduce_grads(params, self.world, self.group)
                 nn.utils.clip_grad_norm_(params, c.max_grad_norm)
                 self.opt.step()
@@ -562,7 +569,7 @@ class PPOTrainer:
                 loss = pg + c.vf_coef * vl - c.ent_coef * ent.mean()
                 self.opt.zero_grad(set_to_none=False)
                 loss.backward()
-                if self.world > 1:
+                if self.collectives:
                     _allreduce_grads(params, self.world, self.group)
                 nn.utils.clip_grad_norm_(params, c.max_grad_norm)
                 self.opt.step()
@@ -584,6 +591,11 @@ class PPOTrainer:
               'gen': self.gen.get_state(), 'obs0': self.buf.obs[0].detach().clone()}
         if hasattr(self.env, 'get_state'):
             sd['env'] = self.env.get_state().detach().clone()
+            if hasattr(self.env, 'state_meta'):
+                sd['env_meta'] = self.env.state_meta()
+        elif hasattr(self.env, 'n_envs') and self.env.__class__.__module__.startswith('masurvival'):
+            raise ValueError(f'{type(self.env).__name__} cannot export its env state (no get_state): '
+                             'a checkpoint without it would not resume the same trajectory')
         return sd
 
     @torch.no_grad()
@@ -596,6 +608,14 @@ class PPOTrainer:
         if 'env' in sd:
             if not hasattr(self.env, 'set_state'):
                 raise ValueError('checkpoint holds an env state but this env has no set_state')
+            want = sd.get('env_meta')
+            have = self.env.state_meta() if hasattr(self.env, 'state_meta') else None
+            if want is not None and have is not None:
+                # a state image only means something for the same config,
+                # capacity class, env count and shard split
+                diff = {k: (want.get(k), have.get(k)) for k in have if want.get(k) != have.get(k)}
+                if diff:
+                    raise ValueError(f'checkpoint env state does not match this env: {diff}')
             self.env.set_state(sd['env'].to(self.device))
         self.buf.obs[0].copy_(sd['obs0'])
         if self.fused is not None:

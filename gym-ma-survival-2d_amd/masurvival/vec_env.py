@@ -214,8 +214,20 @@ class VecMaSurvival:
         return buf
 
     def set_state(self, buf):
-        assert buf.numel() == self.state_bytes() and buf.device == self.device
+        if buf.numel() != self.state_bytes() or buf.device != self.device:
+            raise ValueError(f'env state image of {buf.numel()} bytes, expected {self.state_bytes()} on {self.device}')
+        buf = buf.contiguous()
         check(self._lib.mas_set_state(self._h, ctypes.c_void_p(buf.data_ptr()), self._stream()))
+
+    def state_meta(self):
+        """What a mas_get_state image depends on: the resolved config struct
+        (its bytes, hashed), the number of envs and the image size (which
+        encodes the capacity class and the state stride).  Plain Python values,
+        stored in PPOTrainer checkpoints and compared on load."""
+        import hashlib
+        cfg = bytes(memoryview(self._cfg))
+        return {'config_sha256': hashlib.sha256(cfg).hexdigest(), 'n_envs': self.n_envs, 'shards': [self.n_envs],
+                'state_bytes': self.state_bytes(), 'n_agents': self.n_agents, 'obs_dim': self.obs_dim}
 
     def close(self):
         if getattr(self, '_h', None) is not None and self._h.value:
@@ -299,8 +311,19 @@ class ShardedVecMaSurvival:
         self.join()
         return self.obs
 
-    def step(self, actions, out=None):
+    def step(self, actions, out=None, validate=False):
+        """As VecMaSurvival.step over the shards; validate checks every
+        action against the action space first (the reference's assert,
+        masurvival_env.py:80), otherwise out-of-range entries are clamped on
+        device and counted (:meth:`invalid_actions`)."""
         torch = _torch()
+        N, A = self.n_envs, self.n_agents
+        if tuple(actions.shape) != (N, A, 6):
+            raise ValueError(f'actions must have shape {(N, A, 6)}, got {tuple(actions.shape)}')
+        if validate:
+            hi = torch.tensor([3, 3, 3, 2, 2, 2], device=actions.device)
+            if bool(((actions < 0) | (actions >= hi)).any()):
+                raise AssertionError('Invalid action: outside MultiDiscrete([3, 3, 3, 2, 2, 2])')
         obs, rew, done = (self.obs, self.rewards, self.dones) if out is None else out
         self.fork()
         for e, s, lo, hi in self.shard_slices():
@@ -308,6 +331,11 @@ class ShardedVecMaSurvival:
                 e.step(actions[lo:hi], out=(obs[lo:hi], rew[lo:hi], done[lo:hi]))
         self.join()
         return obs, rew, done, {}
+
+    def invalid_actions(self, reset: bool = True) -> int:
+        """Sum over the shards of VecMaSurvival.invalid_actions (synchronises)."""
+        self.join()
+        return sum(e.invalid_actions(reset) for e in self.envs)
 
     def flush_stats(self):
         self.join()
@@ -323,6 +351,32 @@ class ShardedVecMaSurvival:
 
     def state_bytes(self) -> int:
         return sum(e.state_bytes() for e in self.envs)
+
+    def get_state(self):
+        """The shards' mas_get_state images, concatenated in shard order."""
+        self.join()
+        return _torch().cat([e.get_state() for e in self.envs])
+
+    def set_state(self, buf):
+        """Split a get_state() image at the shards' byte counts and restore
+        each shard from its part."""
+        sizes = [e.state_bytes() for e in self.envs]
+        if buf.numel() != sum(sizes) or buf.device != self.device:
+            raise ValueError(f'env state image of {buf.numel()} bytes, expected {sum(sizes)} on {self.device}')
+        self.join()
+        off = 0
+        for e, n in zip(self.envs, sizes):
+            e.set_state(buf[off:off + n])
+            off += n
+        _torch().cuda.synchronize(self.device)
+
+    def state_meta(self):
+        """What a checkpoint's env state depends on (see VecMaSurvival.state_meta)."""
+        m = self.envs[0].state_meta()
+        m['n_envs'] = self.n_envs
+        m['shards'] = [e.n_envs for e in self.envs]
+        m['state_bytes'] = self.state_bytes()
+        return m
 
     def close(self):
         for e in self.envs:

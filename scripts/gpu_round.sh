@@ -13,6 +13,11 @@ for step in "$@"; do
     tests)
       cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread \
         -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { echo "tests failed"; exit 1; } ;;
+    t:*)
+      # t:<file.py>[,<file.py>...]: those GPU test files only
+      F=$(echo ${step#t:} | tr ',' ' ' | sed 's#\([^ ]*\)#tests/\1#g')
+      cd $R && timeout -k 10 900 python -u -m pytest $F -m gpu -x -v -s --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > $O/gpu_tests_sel.log 2>&1 || { echo "selected tests failed"; exit 1; } ;;
     regimes)
       cd $R && MAS_DUMP_DIR=$O timeout -k 10 900 python -u -m pytest tests/test_gpu_parity_regimes.py -x -v -s \
         --timeout 600 --timeout-method thread -p no:cacheprovider > $O/regimes.log 2>&1 || { echo "regimes failed"; exit 1; } ;;

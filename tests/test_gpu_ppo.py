@@ -89,19 +89,28 @@ def test_sharded_rollout_matches_one_handle():
         t_.env.close()
 
 
-def test_checkpoint_resume_on_env(tmp_path):
+def _vec(n, seeds, shards):
+    if shards == 1:
+        return VecMaSurvival(C3_CONFIG, n_envs=n, seeds=seeds, auto_reset=True)
+    from masurvival.vec_env import ShardedVecMaSurvival
+    return ShardedVecMaSurvival(C3_CONFIG, n_envs=n, shards=shards, seeds=seeds, auto_reset=True)
+
+
+@pytest.mark.parametrize('shards', [1, 2])
+def test_checkpoint_resume_on_env(tmp_path, shards):
     """PPOTrainer.save after an iteration, load into a fresh trainer on a fresh
     env: the next rollout (fused act kernel + env kernels) is bit-identical to
     the run that never stopped -- policy, env state and sampling counters all
-    restored."""
+    restored.  shards=2: the env is a ShardedVecMaSurvival, whose state image
+    is its shards' images concatenated."""
     n, T = 1024, 8
     trs = []
-    env = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n), auto_reset=True)
+    env = _vec(n, list(range(n)), shards)
     tr = PPOTrainer(env, PPOConfig(horizon=T), seed=0)
     tr.iteration()
     path = str(tmp_path / 'ckpt.pt')
     tr.save(path)
-    env2 = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(1000, 1000 + n), auto_reset=True)
+    env2 = _vec(n, list(range(1000, 1000 + n)), shards)
     tr2 = PPOTrainer(env2, PPOConfig(horizon=T), seed=5)
     tr2.load(path)
     for t_ in (tr, tr2):
@@ -117,3 +126,29 @@ def test_checkpoint_resume_on_env(tmp_path):
         assert torch.equal(getattr(b1, name), getattr(b2, name)), name
     env.close()
     env2.close()
+
+
+def test_checkpoint_env_mismatch_is_refused(tmp_path):
+    """A checkpoint's env state only loads into an env with the same config,
+    env count and shard split (same image size is not enough)."""
+    n, T = 256, 4
+    env = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n))
+    tr = PPOTrainer(env, PPOConfig(horizon=T), seed=0)
+    tr.iteration()
+    path = str(tmp_path / 'ckpt.pt')
+    tr.save(path)
+    sb = env.state_bytes()
+    env.close()
+    # same capacity class (2v2) and N, hence the same image size, other config
+    other = dict(C3_CONFIG, melee={'range': 3, 'damage': 20, 'cooldown': 40, 'drift': True})
+    env2 = VecMaSurvival(other, n_envs=n, seeds=range(n))
+    assert env2.state_bytes() == sb
+    tr2 = PPOTrainer(env2, PPOConfig(horizon=T), seed=0)
+    with pytest.raises(ValueError, match='does not match'):
+        tr2.load(path)
+    env2.close()
+    env3 = _vec(n, list(range(n)), 2)
+    tr3 = PPOTrainer(env3, PPOConfig(horizon=T), seed=0)
+    with pytest.raises(ValueError, match='does not match'):
+        tr3.load(path)
+    env3.close()
