@@ -523,8 +523,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
     h->P.prof = nullptr;
     h->phys = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 4) * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 4) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 8) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 8) * sizeof(int));
     h->sweep = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * 8 * sizeof(float));
     h->P.sweep = h->sweep;
@@ -537,6 +537,9 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
     h->P.gen_next = h->phys ? h->phys + n_envs + 2 : nullptr;
     h->P.phys_last = h->phys ? h->phys + n_envs + 3 : nullptr;
+    h->P.list_overflow = h->phys ? h->phys + n_envs + 4 : nullptr;
+    h->P.force_general = 0;
+    h->P.solve_one_lane = 0;
     h->toi = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->toi, ((size_t)2 * n_envs * 8 + 2) * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->toi, 0, ((size_t)2 * n_envs * 8 + 2) * sizeof(int));
@@ -702,6 +705,24 @@ int mas_debug_counters(mas_handle* h, int64_t* host_out)
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(&c, h->P.phys_last, sizeof(int), hipMemcpyDeviceToHost));
     host_out[0] = c;
+    return MAS_OK;
+}
+
+int mas_debug_guards(mas_handle* h, int64_t* host_out)
+{
+    if (!h || !host_out) return fail(MAS_ERR_INVALID_ARG, "mas_debug_guards: null argument");
+    int c = 0;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&c, h->P.list_overflow, sizeof(int), hipMemcpyDeviceToHost));
+    host_out[0] = c;
+    return MAS_OK;
+}
+
+int mas_debug_force_general(mas_handle* h, int32_t on)
+{
+    if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: null handle");
+    h->P.force_general = (on & 1) ? 1 : 0;
+    h->P.solve_one_lane = (on & 2) ? 1 : 0;
     return MAS_OK;
 }
 

@@ -85,6 +85,9 @@ struct Params {
     int* phys_count;  // number of them
     int* gen_next;    // k_gen work queue: next chunk of the list (reset by k_post)
     int* phys_last;   // the list count of the last step (mas_debug_counters; k_post)
+    int* list_overflow;  // appends to phys_list / toi_list refused by their bounds (mas_debug_guards; must stay 0)
+    int force_general;   // test diagnostics (mas_debug_force_general): every env takes the general physics path
+    int solve_one_lane;  // test diagnostics (mas_debug_force_general, on = 2): the one-lane-per-env k_gen_solve
     int* toi_list;    // [2][N * AM] (env, agent) pairs for k_gen_toi, per world step (k_gen_solve)
     int* toi_count;   // [2] their counts (reset by k_post)
     uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)

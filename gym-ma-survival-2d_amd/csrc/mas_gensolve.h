@@ -1,0 +1,562 @@
+// mas_gensolve.h -- b2World::Step Collide + island Solve of the general
+// physics path on a lane group per env (k_gen_solve_g, mas_kernels.inc).
+//
+// Same state changes, bit for bit, as world_step_solve (mas_physics.h) --
+// the one-lane-per-env form this replaces, itself the restatement of
+// b2World::Step up to SolveTOI (Box2D 2.3.x b2World::Solve, b2Island::Solve,
+// b2ContactSolver) that oracle/mas_oracle.c pins:
+//
+//   Collide   agent-agent pairs: few and order-dependent (a wake makes a
+//             later pair of the same agent eligible), so every lane of the
+//             group runs the short pair loop on the same values; lane p
+//             writes pair p's impulse reset.  Agent-static pairs: lane s of
+//             the group owns static s and updates (agent i, s) for every
+//             awake agent i -- the AABB cull, b2CollidePolygonAndCircle and
+//             the impulse reset on its lane; a wave ballot per agent gives
+//             the new touching word.  (An agent-static update only wakes an
+//             agent that is already awake, so these pairs are independent.)
+//   Solve     every lane labels the islands (uniform).  The velocity
+//             constraints are initialised in parallel, each on the lane that
+//             owns the contact (lane p: agent pair p; lane s: agent-static
+//             pairs of static s), and written to LDS at the contact's
+//             canonical index (agent-agent i<j, then agent-static
+//             agent-major, statics ascending: ballot + popcount prefix).
+//             Lane r (agent r) then runs b2Island::Solve for the island it
+//             roots: warm start, 10 velocity iterations, impulse store,
+//             integration, <= 10 position iterations with the island's
+//             early exit, sleep.  Islands share no body and no contact, so
+//             solving them apart, each in canonical order, is solving them
+//             together; the Gauss-Seidel loops stop at an exact fixed point
+//             (same_bits, mas_physics.h), per island.
+//
+// A group is G lanes (G >= statics, agent pairs and agents), 64 / G envs per
+// wave, over the compacted general-path list: where the one-lane kernel ran
+// every flagged env's serial Collide (A x (B + 4) pairs) and whole-env solve
+// on one lane, a wave here waits for its slowest island.
+#pragma once
+
+#include "mas_step.h"
+
+namespace mas {
+
+template <class C>
+struct SolveShape {
+    static constexpr int need0 = C::NS > C::NAA ? C::NS : C::NAA;
+    static constexpr int need = need0 > C::AM ? need0 : C::AM;
+    static constexpr int G = need <= 8 ? 8 : (need <= 16 ? 16 : 32);  // lanes per env
+    static constexpr int EPW = kWG / G;                               // envs per wave
+    static constexpr int KL = C::NAA + C::AM * C::NS;                 // contact records per env
+    static_assert(need <= 32, "one lane per static / agent pair, 32-bit group ballots");
+};
+
+// contact record fields in LDS ([field][q][env of the wave])
+enum {
+    kRnx, kRny, kRax, kRay, kRbx, kRby, kRnm, kRtm,  // VC: normal, rA, rB, normal / tangent mass
+    kRni, kRti,                                      // accumulated impulses (warm-started)
+    kRkey,                                           // type << 16 | i << 8 | j-or-static (slot_* helpers)
+    kRpnx, kRpny, kRppx, kRppy,                      // agent-static: world normal / plane point (position solve)
+    kRecW
+};
+
+template <class C>
+struct SolveRec {
+    float* f;
+    int slot;
+    __device__ __forceinline__ float& at(int field, int q) const
+    {
+        return f[(field * SolveShape<C>::KL + q) * SolveShape<C>::EPW + slot];
+    }
+};
+
+// ballot bits of this lane's group (group-relative lane order)
+template <int G>
+__device__ __forceinline__ uint32_t group_ballot(bool b)
+{
+    const int base = (int)(threadIdx.x & 63) & ~(G - 1);
+    const uint64_t m = __ballot(b);
+    return (uint32_t)((m >> base) & ((1ull << G) - 1ull));
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_or(uint32_t v)
+{
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
+// static s's body (walls 0..3 from P, box s-4 from its state words) and its
+// world AABB (world_step_solve's cull)
+template <class C>
+__device__ __forceinline__ void group_static(const Params& P, const uint32_t* __restrict__ state, int64_t N, int64_t e,
+                                             bool load, int s, StaticG& g, V2& lo, V2& hi)
+{
+    if (s < kNumWalls) {
+        V2 wp = opq(P.wall_pos[0]), wl = opq(P.wall_lo[0]), wh = opq(P.wall_hi[0]);
+        Rot wq = P.wall_q[0];
+        float wa = P.wall_angle[0];
+#pragma unroll
+        for (int k = 1; k < kNumWalls; ++k)
+            if (s == k) {
+                wp = opq(P.wall_pos[k]);
+                wl = opq(P.wall_lo[k]);
+                wh = opq(P.wall_hi[k]);
+                wq.s = opq(P.wall_q[k].s);
+                wq.c = opq(P.wall_q[k].c);
+                wa = opq(P.wall_angle[k]);
+            }
+        g.p = wp;
+        g.q = wq;
+        g.angle = wa;
+        g.poly = P.wall_poly;
+        lo = wl;
+        hi = wh;
+    } else {
+        using TW = StateWords<C>;
+        const int b = s - kNumWalls < C::BM ? s - kNumWalls : C::BM - 1;
+        const int wb = TW::box + 1 + 6 * b;
+        V2 bp = mk(0.0f, 0.0f);
+        float hx = 0.0f, hy = 0.0f;
+        int meta = 0;
+        if (load) {
+            bp = mk(__uint_as_float(state[state_index(wb, e, N)]), __uint_as_float(state[state_index(wb + 1, e, N)]));
+            hx = __uint_as_float(state[state_index(wb + 2, e, N)]);
+            hy = __uint_as_float(state[state_index(wb + 3, e, N)]);
+            meta = (int)state[state_index(wb + 4, e, N)];
+        }
+        g.p = bp;
+        g.q = kIdRot;
+        g.angle = 0.0f;
+        g.poly = box_poly(hx, hy, box_rot(meta), box_copied(meta));
+        lo = mk(bp.x - hx, bp.y - hy);
+        hi = mk(bp.x + hx, bp.y + hy);
+    }
+}
+
+// One world step's Collide + Solve of env e on this lane's group (lane s of
+// the group).  valid: the group holds an env (every lane of the wave runs the
+// ballots and the barrier).  rec: this workgroup's contact records.
+template <class C>
+__device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __restrict__ state, int64_t N, int64_t e,
+                                                bool valid, int s, float* rec_lds, int slot)
+{
+    using SS = SolveShape<C>;
+    using TW = StateWords<C>;
+    constexpr int G = SS::G, AM = C::AM, NS = C::NS, NAA = C::NAA;
+    const float dt = (float)(1.0 / 60.0);
+    const float m = P.inv_mass, Ii = P.inv_I;
+    const Cont<C, ContGlbStore<C>> K{{state, N, e, P.w_cont}};
+    const SolveRec<C> R{rec_lds, slot};
+
+    // ---------------- load: the agents (every lane), this lane's static ----------------
+    V2 c[AM], v[AM];
+    float a[AM], w[AM], sl[AM];
+    uint32_t alive = 0, awake = 0, aat0 = 0, ast0[AM];
+    int nbox = 0;
+    float inv_dt0 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        c[i] = v[i] = mk(0.0f, 0.0f);
+        a[i] = w[i] = sl[i] = 0.0f;
+        ast0[i] = 0u;
+    }
+    if (valid) {
+#pragma unroll
+        for (int i = 0; i < AM; ++i) {
+            c[i] = mk(__uint_as_float(state[state_index(7 * i, e, N)]), __uint_as_float(state[state_index(7 * i + 1, e, N)]));
+            a[i] = __uint_as_float(state[state_index(7 * i + 2, e, N)]);
+            v[i] = mk(__uint_as_float(state[state_index(7 * i + 3, e, N)]), __uint_as_float(state[state_index(7 * i + 4, e, N)]));
+            w[i] = __uint_as_float(state[state_index(7 * i + 5, e, N)]);
+            sl[i] = __uint_as_float(state[state_index(7 * i + 6, e, N)]);
+        }
+        alive = state[state_index(TW::alive, e, N)];
+        awake = state[state_index(TW::awake, e, N)];
+        nbox = (int)state[state_index(TW::box, e, N)];
+        inv_dt0 = __uint_as_float(state[state_index(P.w_invdt, e, N)]);
+        aat0 = K.aat();
+#pragma unroll
+        for (int i = 0; i < AM; ++i) ast0[i] = K.ast(i);
+    }
+    V2 cs[AM];  // sweep start (b2Sweep c0) = the positions before the solve
+    float as_[AM];
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        cs[i] = c[i];
+        as_[i] = a[i];
+    }
+    const int sc = s < NS ? s : NS - 1;
+    StaticG g;
+    V2 lo, hi;
+    group_static<C>(P, state, N, e, valid && s < NS && s >= kNumWalls, sc, g, lo, hi);
+    const float inv_dt = 1.0f / dt;
+    const float dtRatio = inv_dt0 * dt;
+    MAS_PROF(P, kPfLoad);
+
+    // ---------------- Collide: agent-agent pairs (serial on every lane) ----------------
+    uint32_t aat = aat0, aa_eval = 0;
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = i + 1; j < AM; ++j) {
+            if (!(bit(alive, i) && bit(alive, j))) continue;
+            if (!(bit(awake, i) || bit(awake, j))) continue;
+            const int p = aa_index<AM>(i, j);
+            const bool was = bit(aat, p);
+            const V2 d = sub(c[j], c[i]);
+            const float dsq = dot(d, d);
+            const float rad = P.agent_r + P.agent_r;
+            const bool touching = !(dsq > rad * rad);
+            aa_eval |= 1u << p;
+            // impulses reset (b2Contact::Update): a pair that stays out of
+            // contact here; a new contact's reset is folded into its warm
+            // start below (the solve writes its impulses)
+            if (valid && s == p && !touching) {
+                K.set_aani(p, 0.0f);
+                K.set_aati(p, 0.0f);
+            }
+            aat = touching ? (aat | (1u << p)) : (aat & ~(1u << p));
+            if (touching != was) {
+                if (!bit(awake, i)) { awake |= 1u << i; sl[i] = 0.0f; }
+                if (!bit(awake, j)) { awake |= 1u << j; sl[j] = 0.0f; }
+            }
+        }
+
+    // ---------------- Collide: agent-static pairs, static s on lane s ----------------
+    const int ns = kNumWalls + nbox;
+    const float reach = P.agent_r + kPolyRadius + 1e-3f;
+    uint32_t my_t = 0, my_lost = 0, my_new = 0;  // bit i: agent i's pair with this static
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        const bool ev = valid && s < ns && bit(alive, i) && bit(awake, i);
+        const bool was = bit(ast0[i], s);
+        const float dx = fmaxf(fmaxf(lo.x - c[i].x, c[i].x - hi.x), 0.0f);
+        const float dy = fmaxf(fmaxf(lo.y - c[i].y, c[i].y - hi.y), 0.0f);
+        const bool cand = dx * dx + dy * dy <= reach * reach;
+        bool t = false;
+        if (ev && cand) {
+            V2 ln, lp;
+            t = collide_pc(g.poly, g.p, g.q, c[i], kPolyRadius, P.agent_r, ln, lp);
+        }
+        if (ev && !t && (was || cand)) {
+            K.set_asni(i, s, 0.0f);
+            K.set_asti(i, s, 0.0f);
+        }
+        if (t) my_t |= 1u << i;
+        if (ev && was && !cand) my_lost |= 1u << i;
+        if (ev && t && !was) my_new |= 1u << i;
+    }
+    uint32_t ast[AM];
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        const uint32_t tb = group_ballot<G>(bit(my_t, i));
+        const bool lost = group_ballot<G>(bit(my_lost, i)) != 0u;
+        const uint32_t low = ns >= 32 ? 0xffffffffu : ((1u << ns) - 1u);
+        const bool ev = bit(alive, i) && bit(awake, i);
+        ast[i] = ev ? ((lost ? 0u : (ast0[i] & ~low)) | tb) : ast0[i];
+    }
+    MAS_PROF(P, kPfCollide);
+
+    // ---------------- Solve: islands (uniform), wake, damping ----------------
+    int label[AM];
+#pragma unroll
+    for (int i = 0; i < AM; ++i) label[i] = i;
+#pragma unroll
+    for (int pass = 0; pass < AM; ++pass) {
+        if (aat == 0u) break;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = i + 1; j < AM; ++j) {
+                const int p = aa_index<AM>(i, j);
+                if (bit(alive, i) && bit(alive, j) && bit(aat, p)) {
+                    const int l = label[i] < label[j] ? label[i] : label[j];
+                    label[i] = l;
+                    label[j] = l;
+                }
+            }
+    }
+    uint32_t solved = 0;
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < AM; ++j)
+            if (label[j] == label[i] && bit(alive, j) && bit(awake, j)) any = true;
+        if (bit(alive, i) && any) solved |= 1u << i;
+    }
+    if (!valid) solved = 0;
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+        if (bit(solved, i) && !bit(awake, i)) {
+            awake |= 1u << i;
+            sl[i] = 0.0f;
+        }
+    const uint32_t awake_pre = awake;
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        if (!bit(solved, i)) continue;
+        const float ld = 1.0f / (1.0f + dt * P.lin_damp);
+        v[i].x *= ld;
+        v[i].y *= ld;
+        const float ad = 1.0f / (1.0f + dt * P.ang_damp);
+        w[i] *= ad;
+    }
+
+    // ---------------- contact list: canonical index, velocity constraints ----------------
+    uint32_t aa_list = 0;
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = i + 1; j < AM; ++j)
+            if (bit(solved, i) && bit(solved, j) && bit(aat, aa_index<AM>(i, j))) aa_list |= 1u << aa_index<AM>(i, j);
+    const uint32_t nsmask = NS >= 32 ? 0xffffffffu : ((1u << NS) - 1u);
+    int before[AM], nq = __popc(aa_list);
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        before[i] = nq;
+        if (bit(solved, i)) nq += __popc(ast[i] & nsmask);
+    }
+    // agent-agent contact p on lane p
+    if (s < NAA && bit(aa_list, s)) {
+        int pi = 0, pj = 1;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+            for (int j = i + 1; j < AM; ++j)
+                if (aa_index<AM>(i, j) == s) { pi = i; pj = j; }
+        const bool reset = bit(aa_eval, s) && !bit(aat0, s);
+        const float sni = reset ? 0.0f : K.aani(s), sti = reset ? 0.0f : K.aati(s);
+        VC k = vc_init_aa(sel(c, pi), sel(c, pj), P.agent_r, m, Ii, m, Ii);
+        k.ni = dtRatio * sni;
+        k.ti = dtRatio * sti;
+        const int q = __popc(aa_list & ((1u << s) - 1u));
+        R.at(kRnx, q) = k.normal.x; R.at(kRny, q) = k.normal.y;
+        R.at(kRax, q) = k.rA.x; R.at(kRay, q) = k.rA.y;
+        R.at(kRbx, q) = k.rB.x; R.at(kRby, q) = k.rB.y;
+        R.at(kRnm, q) = k.nm; R.at(kRtm, q) = k.tm;
+        R.at(kRni, q) = k.ni; R.at(kRti, q) = k.ti;
+        R.at(kRkey, q) = __int_as_float((0 << 16) | (pi << 8) | pj);
+    }
+    // agent-static contacts of static s on lane s
+    if (s < NS) {
+#pragma unroll
+        for (int i = 0; i < AM; ++i) {
+            if (!(bit(solved, i) && bit(ast[i], s))) continue;
+            V2 ln = mk(0.0f, 0.0f), lp = mk(0.0f, 0.0f);
+            collide_pc(g.poly, g.p, g.q, c[i], kPolyRadius, P.agent_r, ln, lp);
+            VC k = vc_init_as(g.p, g.q, ln, lp, c[i], P.agent_r, m, Ii);
+            const bool reset = bit(my_new, i);
+            const float sni = reset ? 0.0f : K.asni(i, s), sti = reset ? 0.0f : K.asti(i, s);
+            k.ni = dtRatio * sni;
+            k.ti = dtRatio * sti;
+            const int q = before[i] + __popc(ast[i] & ((1u << s) - 1u));
+            const V2 pn = rmul(g.q, ln), pp = xmul(g.p, g.q, lp);
+            R.at(kRnx, q) = k.normal.x; R.at(kRny, q) = k.normal.y;
+            R.at(kRax, q) = k.rA.x; R.at(kRay, q) = k.rA.y;
+            R.at(kRbx, q) = k.rB.x; R.at(kRby, q) = k.rB.y;
+            R.at(kRnm, q) = k.nm; R.at(kRtm, q) = k.tm;
+            R.at(kRni, q) = k.ni; R.at(kRti, q) = k.ti;
+            R.at(kRkey, q) = __int_as_float((1 << 16) | (i << 8) | s);
+            R.at(kRpnx, q) = pn.x; R.at(kRpny, q) = pn.y;
+            R.at(kRppx, q) = pp.x; R.at(kRppy, q) = pp.y;
+        }
+    }
+    __syncthreads();  // the records are in LDS (the workgroup is this wave)
+
+    // ---------------- b2Island::Solve of the island agent s roots ----------------
+    uint32_t new_awake = 0;  // this root's members' awake bits after sleep
+    const bool root = s < AM && bit(solved, s) && sel(label, s) == s;
+    if (root) {
+        const int r = s;
+        uint32_t members = 0;
+#pragma unroll
+        for (int j = 0; j < AM; ++j)
+            if (label[j] == r && bit(solved, j)) members |= 1u << j;
+        auto mine = [&](int q, int& key) {
+            key = __float_as_int(R.at(kRkey, q));
+            return sel(label, slot_i(key)) == r;
+        };
+        auto load_vc = [&](int q) {
+            VC k;
+            k.normal = mk(R.at(kRnx, q), R.at(kRny, q));
+            k.rA = mk(R.at(kRax, q), R.at(kRay, q));
+            k.rB = mk(R.at(kRbx, q), R.at(kRby, q));
+            k.nm = R.at(kRnm, q);
+            k.tm = R.at(kRtm, q);
+            k.ni = R.at(kRni, q);
+            k.ti = R.at(kRti, q);
+            return k;
+        };
+        // warm start
+#pragma unroll 1
+        for (int q = 0; q < nq; ++q) {
+            int key;
+            if (!mine(q, key)) continue;
+            const VC k = load_vc(q);
+            const int i = slot_i(key), js = slot_js(key);
+            V2 vA = mk(0.0f, 0.0f), vB;
+            float wA = 0.0f, wB;
+            if (slot_type(key) == 0) {
+                vA = sel(v, i); wA = sel(w, i);
+                vB = sel(v, js); wB = sel(w, js);
+                vc_warm(k, vA, wA, vB, wB, m, Ii, m, Ii);
+                put(v, i, vA); put(w, i, wA);
+                put(v, js, vB); put(w, js, wB);
+            } else {
+                vB = sel(v, i); wB = sel(w, i);
+                vc_warm(k, vA, wA, vB, wB, 0.0f, 0.0f, m, Ii);
+                put(v, i, vB); put(w, i, wB);
+            }
+        }
+        // velocity iterations (exact fixed-point exit, per island)
+#pragma unroll 1
+        for (int it = 0; it < 10; ++it) {
+            V2 vp[AM];
+            float wp[AM];
+#pragma unroll
+            for (int j = 0; j < AM; ++j) {
+                vp[j] = v[j];
+                wp[j] = w[j];
+            }
+            bool same = true;
+#pragma unroll 1
+            for (int q = 0; q < nq; ++q) {
+                int key;
+                if (!mine(q, key)) continue;
+                VC k = load_vc(q);
+                const float ni0 = k.ni, ti0 = k.ti;
+                const int i = slot_i(key), js = slot_js(key);
+                V2 vA = mk(0.0f, 0.0f), vB;
+                float wA = 0.0f, wB;
+                if (slot_type(key) == 0) {
+                    vA = sel(v, i); wA = sel(w, i);
+                    vB = sel(v, js); wB = sel(w, js);
+                    vc_solve(k, vA, wA, vB, wB, m, Ii, m, Ii);
+                    put(v, i, vA); put(w, i, wA);
+                    put(v, js, vB); put(w, js, wB);
+                } else {
+                    vB = sel(v, i); wB = sel(w, i);
+                    vc_solve(k, vA, wA, vB, wB, 0.0f, 0.0f, m, Ii);
+                    put(v, i, vB); put(w, i, wB);
+                }
+                same = same && same_bits(k.ni, ni0) && same_bits(k.ti, ti0);
+                R.at(kRni, q) = k.ni;
+                R.at(kRti, q) = k.ti;
+            }
+#pragma unroll
+            for (int j = 0; j < AM; ++j) same = same && same_bits(v[j], vp[j]) && same_bits(w[j], wp[j]);
+            if (same) break;
+        }
+        // store impulses
+#pragma unroll 1
+        for (int q = 0; q < nq; ++q) {
+            int key;
+            if (!mine(q, key)) continue;
+            const int i = slot_i(key), js = slot_js(key);
+            const float ni = R.at(kRni, q), ti = R.at(kRti, q);
+            if (slot_type(key) == 0) {
+                const int p = aa_index<AM>(i, js);
+                K.set_aani(p, ni);
+                K.set_aati(p, ti);
+            } else {
+                K.set_asni(i, js, ni);
+                K.set_asti(i, js, ti);
+            }
+        }
+        // integrate positions
+#pragma unroll
+        for (int j = 0; j < AM; ++j)
+            if (bit(members, j)) integrate(c[j], a[j], v[j], w[j], dt);
+        // position iterations, the island's early exit
+        bool converged = false;
+#pragma unroll 1
+        for (int it = 0; it < 10; ++it) {
+            float minsep = 0.0f;
+#pragma unroll 1
+            for (int q = 0; q < nq; ++q) {
+                int key;
+                if (!mine(q, key)) continue;
+                const int i = slot_i(key), js = slot_js(key);
+                float sep;
+                if (slot_type(key) == 0) {
+                    V2 cA = sel(c, i), cB = sel(c, js);
+                    float aA = sel(a, i), aB = sel(a, js);
+                    sep = pc_solve_aa(cA, aA, cB, aB, P.agent_r, m, Ii, kBaumgarte);
+                    put(c, i, cA); put(a, i, aA);
+                    put(c, js, cB); put(a, js, aB);
+                } else {
+                    const V2 pn = mk(R.at(kRpnx, q), R.at(kRpny, q)), pp = mk(R.at(kRppx, q), R.at(kRppy, q));
+                    V2 cB = sel(c, i);
+                    float aB = sel(a, i);
+                    sep = pc_solve_as_h(pn, pp, cB, aB, P.agent_r, m, Ii, kBaumgarte, P.inv_mass_rcp);
+                    put(c, i, cB); put(a, i, aB);
+                }
+                minsep = fmin_b2(minsep, sep);
+            }
+            if (minsep >= -3.0f * kLinearSlop) {
+                converged = true;
+                break;
+            }
+        }
+        // sleep (per island)
+        const float linTolSqr = kLinSleepTol * kLinSleepTol;
+        const float angTolSqr = kAngSleepTol * kAngSleepTol;
+        // (branch-free: the short-circuit if / else form of this loop was
+        // miscompiled for the 1v1 class -- on the "w small, v large" path the
+        // register holding sl[j] = 0 was reused for v.y^2 and stored as the
+        // sleep time; scripts/ab_solve_golden.py found it)
+        float ms = kMaxFloat;
+#pragma unroll
+        for (int j = 0; j < AM; ++j) {
+            const float ww = w[j] * w[j], vv = dot(v[j], v[j]);
+            const bool moving = (ww > angTolSqr) | (vv > linTolSqr);
+            const float acc = opq(sl[j] + dt);
+            const bool mem = bit(members, j);
+            sl[j] = mem ? (moving ? 0.0f : acc) : sl[j];
+            ms = mem ? (moving ? 0.0f : fmin_b2(ms, acc)) : ms;
+        }
+        new_awake = members;
+        if (ms >= kTimeToSleep && converged) {
+            new_awake = 0;
+#pragma unroll
+            for (int j = 0; j < AM; ++j) {
+                if (!bit(members, j)) continue;
+                sl[j] = 0.0f;
+                v[j] = mk(0.0f, 0.0f);
+                w[j] = 0.0f;
+            }
+        }
+        // the island's bodies (b2Island::Solve writes back every member)
+#pragma unroll
+        for (int j = 0; j < AM; ++j) {
+            if (!bit(members, j)) continue;
+            const float out[7] = {c[j].x, c[j].y, a[j], v[j].x, v[j].y, w[j], sl[j]};
+#pragma unroll
+            for (int q = 0; q < 7; ++q) state[state_index(7 * j + q, e, N)] = __float_as_uint(out[q]);
+        }
+    }
+    MAS_PROF(P, kPfSolve);
+    const uint32_t awake_fin = (awake_pre & ~solved) | group_or<G>(new_awake);
+    if (!valid) return;
+    // touching words, awake mask, b2World's previous 1/dt, the sweep starts
+    if (s == 0) {
+        if (aat != aat0) K.set_aat(aat);
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+            if (ast[i] != ast0[i]) K.set_ast(i, ast[i]);
+        state[state_index(TW::awake, e, N)] = awake_fin;
+        state[state_index(P.w_invdt, e, N)] = __float_as_uint(inv_dt);
+    }
+    // agents woken by Collide that no island holds cannot exist (a woken agent
+    // is alive and awake, so its island is solved); the sweep of agent s
+    if (s < AM) {
+        float* sw = P.sweep + e * (3 * AM) + 3 * s;
+        const V2 c0s = sel(cs, s);
+        sw[0] = c0s.x;
+        sw[1] = c0s.y;
+        sw[2] = sel(as_, s);
+    }
+    MAS_PROF(P, kPfStore);
+}
+
+}  // namespace mas

@@ -63,6 +63,8 @@ SIGNATURES = {
     'mas_gae': (c_int32, [c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
                           c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
+    'mas_debug_guards': (c_int32, [c_void_p, POINTER(c_int64)]),
+    'mas_debug_force_general': (c_int32, [c_void_p, c_int32]),
     'mas_invalid_actions': (c_int32, [c_void_p, POINTER(c_int64), c_int32]),
     'mas_debug_gen_flags': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'mas_debug_set_toi_counter': (c_int32, [c_void_p, c_void_p]),

@@ -171,6 +171,20 @@ class VecMaSurvival:
         check(self._lib.mas_debug_counters(self._h, out))
         return {'phys_general_envs': int(out[0])}
 
+    def debug_guards(self):
+        """{'list_overflow': appends to the general-path / SolveTOI lists that
+        their bounds refused (0 unless a kernel breaks the list invariant)};
+        synchronises."""
+        out = (ctypes.c_int64 * 1)()
+        check(self._lib.mas_debug_guards(self._h, out))
+        return {'list_overflow': int(out[0])}
+
+    def force_general(self, on: bool = True, one_lane_solve: bool = False):
+        """Test diagnostics: every env takes the general physics path (on);
+        one_lane_solve: the general path's Collide + Solve runs one lane per
+        env (k_gen_solve) instead of on lane groups (k_gen_solve_g)."""
+        check(self._lib.mas_debug_force_general(self._h, int(bool(on)) | (2 if one_lane_solve else 0)))
+
     def invalid_actions(self, reset: bool = True) -> int:
         """Env-steps whose actions were out of range (clamped on device) since
         the last reset of the count (mas_invalid_actions; synchronises)."""

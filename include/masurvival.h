@@ -260,6 +260,20 @@ int mas_policy_dw(int32_t f, int32_t g, int64_t k, const void* a, int64_t lda, c
  * physics kernel (contacts, TOI events, box despawns). */
 int mas_debug_counters(mas_handle* h, int64_t* host_out);
 
+/* Diagnostics (synchronises the device): host_out[0] = appends to the
+ * general-path env list (and the optional SolveTOI list) that their bounds
+ * refused since mas_create.  The lists hold one entry per env (per (env,
+ * agent)) and are emptied every step, so this is 0 unless a kernel breaks
+ * that invariant; the tests assert it. */
+int mas_debug_guards(mas_handle* h, int64_t* host_out);
+
+/* Test diagnostics: bit 0 of `on` sends every env of every following
+ * mas_step through the general physics path (the contact-free fast path
+ * gives up for all envs); bit 1 runs the general path's Collide + Solve one
+ * lane per env (k_gen_solve) instead of on lane groups (k_gen_solve_g).
+ * Results are unchanged (every path is exact): A/B and parity tests only. */
+int mas_debug_force_general(mas_handle* h, int32_t on);
+
 /* Action validation.  The reference asserts action_space.contains(actions)
  * before every step (masurvival_env.py:80).  A kernel cannot raise, so
  * mas_step clamps each out-of-range entry into MultiDiscrete([3,3,3,2,2,2])

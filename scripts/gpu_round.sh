@@ -18,6 +18,8 @@ for step in "$@"; do
       F=$(echo ${step#t:} | tr ',' ' ' | sed 's#\([^ ]*\)#tests/\1#g')
       cd $R && timeout -k 10 900 python -u -m pytest $F -m gpu -x -v -s --timeout 300 --timeout-method thread \
         -p no:cacheprovider > $O/gpu_tests_sel.log 2>&1 || { echo "selected tests failed"; exit 1; } ;;
+    ab)
+      cd $R && timeout -k 10 600 python -u scripts/ab_solve_golden.py all > $O/ab_golden.log 2>&1 || { echo "A/B differs"; exit 1; } ;;
     regimes)
       cd $R && MAS_DUMP_DIR=$O timeout -k 10 900 python -u -m pytest tests/test_gpu_parity_regimes.py -x -v -s \
         --timeout 600 --timeout-method thread -p no:cacheprovider > $O/regimes.log 2>&1 || { echo "regimes failed"; exit 1; } ;;
