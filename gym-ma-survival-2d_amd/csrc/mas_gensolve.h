@@ -89,8 +89,11 @@ __device__ __forceinline__ uint32_t group_or(uint32_t v)
 // world AABB (world_step_solve's cull)
 template <class C>
 __device__ __forceinline__ void group_static(const Params& P, const uint32_t* __restrict__ state, int64_t N, int64_t e,
-                                             bool load, int s, StaticG& g, V2& lo, V2& hi)
+                                             bool load, int s, StaticG& g, V2& lo, V2& hi, float& bhx, float& bhy,
+                                             int& bmeta)
 {
+    bhx = bhy = 0.0f;
+    bmeta = 0;
     if (s < kNumWalls) {
         V2 wp = opq(P.wall_pos[0]), wl = opq(P.wall_lo[0]), wh = opq(P.wall_hi[0]);
         Rot wq = P.wall_q[0];
@@ -128,21 +131,177 @@ __device__ __forceinline__ void group_static(const Params& P, const uint32_t* __
         g.q = kIdRot;
         g.angle = 0.0f;
         g.poly = box_poly(hx, hy, box_rot(meta), box_copied(meta));
+        bhx = hx;
+        bhy = hy;
+        bmeta = meta;
         lo = mk(bp.x - hx, bp.y - hy);
         hi = mk(bp.x + hx, bp.y + hy);
+    }
+}
+
+// b2Island::Solve of one island whose n <= KC contacts (record indices qi,
+// canonical order) are held in registers: warm start, 10 velocity
+// iterations (exact fixed-point exit), impulse store, integration, <= 10
+// position iterations with the island's early exit, sleep.  The same
+// operations in the same order as the LDS loops of gen_solve_group (and as
+// world_solve, mas_physics.h).  new_awake: the members still awake.
+template <class C, class KT>
+__device__ __forceinline__ void island_solve_regs(const Params& P, const SolveRec<C>& R, const KT& K,
+                                                  const int (&qi)[C::KC], int n, uint32_t members, V2 (&c)[C::AM],
+                                                  float (&a)[C::AM], V2 (&v)[C::AM], float (&w)[C::AM],
+                                                  float (&sl)[C::AM], float dt, uint32_t& new_awake)
+{
+    constexpr int KC = C::KC, AM = C::AM;
+    const float m = P.inv_mass, Ii = P.inv_I;
+    VC k[KC];
+    int key[KC];
+    V2 pn[KC], pp[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        const int q = j < n ? qi[j] : 0;
+        k[j].normal = mk(R.at(kRnx, q), R.at(kRny, q));
+        k[j].rA = mk(R.at(kRax, q), R.at(kRay, q));
+        k[j].rB = mk(R.at(kRbx, q), R.at(kRby, q));
+        k[j].nm = R.at(kRnm, q);
+        k[j].tm = R.at(kRtm, q);
+        k[j].ni = R.at(kRni, q);
+        k[j].ti = R.at(kRti, q);
+        key[j] = __float_as_int(R.at(kRkey, q));
+        pn[j] = mk(R.at(kRpnx, q), R.at(kRpny, q));
+        pp[j] = mk(R.at(kRppx, q), R.at(kRppy, q));
+    }
+    // one contact's velocity step (warm start or solve) on the bodies
+    auto vel = [&](int j, bool warm) {
+        const int i = slot_i(key[j]), js = slot_js(key[j]);
+        V2 vA = mk(0.0f, 0.0f), vB;
+        float wA = 0.0f, wB;
+        if (slot_type(key[j]) == 0) {
+            vA = sel(v, i); wA = sel(w, i);
+            vB = sel(v, js); wB = sel(w, js);
+            if (warm) vc_warm(k[j], vA, wA, vB, wB, m, Ii, m, Ii);
+            else vc_solve(k[j], vA, wA, vB, wB, m, Ii, m, Ii);
+            put(v, i, vA); put(w, i, wA);
+            put(v, js, vB); put(w, js, wB);
+        } else {
+            vB = sel(v, i); wB = sel(w, i);
+            if (warm) vc_warm(k[j], vA, wA, vB, wB, 0.0f, 0.0f, m, Ii);
+            else vc_solve(k[j], vA, wA, vB, wB, 0.0f, 0.0f, m, Ii);
+            put(v, i, vB); put(w, i, wB);
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < KC; ++j)
+        if (j < n) vel(j, true);
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        V2 vp[AM];
+        float wp[AM], qn[KC], qt[KC];
+#pragma unroll
+        for (int j = 0; j < AM; ++j) {
+            vp[j] = v[j];
+            wp[j] = w[j];
+        }
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            qn[j] = k[j].ni;
+            qt[j] = k[j].ti;
+        }
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+            if (j < n) vel(j, false);
+        bool same = true;
+#pragma unroll
+        for (int j = 0; j < AM; ++j) same = same && same_bits(v[j], vp[j]) && same_bits(w[j], wp[j]);
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+            if (j < n) same = same && same_bits(k[j].ni, qn[j]) && same_bits(k[j].ti, qt[j]);
+        if (same) break;
+    }
+    // store impulses
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        if (j >= n) continue;
+        const int i = slot_i(key[j]), js = slot_js(key[j]);
+        if (slot_type(key[j]) == 0) {
+            const int p = aa_index<AM>(i, js);
+            K.set_aani(p, k[j].ni);
+            K.set_aati(p, k[j].ti);
+        } else {
+            K.set_asni(i, js, k[j].ni);
+            K.set_asti(i, js, k[j].ti);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < AM; ++j)
+        if (bit(members, j)) integrate(c[j], a[j], v[j], w[j], dt);
+    bool converged = false;
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        float minsep = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            if (j >= n) continue;
+            const int i = slot_i(key[j]), js = slot_js(key[j]);
+            float sep;
+            if (slot_type(key[j]) == 0) {
+                V2 cA = sel(c, i), cB = sel(c, js);
+                float aA = sel(a, i), aB = sel(a, js);
+                sep = pc_solve_aa(cA, aA, cB, aB, P.agent_r, m, Ii, kBaumgarte);
+                put(c, i, cA); put(a, i, aA);
+                put(c, js, cB); put(a, js, aB);
+            } else {
+                V2 cB = sel(c, i);
+                float aB = sel(a, i);
+                sep = pc_solve_as_h(pn[j], pp[j], cB, aB, P.agent_r, m, Ii, kBaumgarte, P.inv_mass_rcp);
+                put(c, i, cB); put(a, i, aB);
+            }
+            minsep = fmin_b2(minsep, sep);
+        }
+        if (minsep >= -3.0f * kLinearSlop) {
+            converged = true;
+            break;
+        }
+    }
+    // sleep (branch-free: see gen_solve_group)
+    const float linTolSqr = kLinSleepTol * kLinSleepTol;
+    const float angTolSqr = kAngSleepTol * kAngSleepTol;
+    float ms = kMaxFloat;
+#pragma unroll
+    for (int j = 0; j < AM; ++j) {
+        const float ww = w[j] * w[j], vv = dot(v[j], v[j]);
+        const bool moving = (ww > angTolSqr) | (vv > linTolSqr);
+        const float acc = opq(sl[j] + dt);
+        const bool mem = bit(members, j);
+        sl[j] = mem ? (moving ? 0.0f : acc) : sl[j];
+        ms = mem ? (moving ? 0.0f : fmin_b2(ms, acc)) : ms;
+    }
+    new_awake = members;
+    if (ms >= kTimeToSleep && converged) {
+        new_awake = 0;
+#pragma unroll
+        for (int j = 0; j < AM; ++j) {
+            if (!bit(members, j)) continue;
+            sl[j] = 0.0f;
+            v[j] = mk(0.0f, 0.0f);
+            w[j] = 0.0f;
+        }
     }
 }
 
 // One world step's Collide + Solve of env e on this lane's group (lane s of
 // the group).  valid: the group holds an env (every lane of the wave runs the
 // ballots and the barrier).  rec: this workgroup's contact records.
-template <class C>
+// TOI: also run b2World::SolveTOI of the step on the group (toi_agent_group,
+// mas_physics.h: lane s owns static s) -- the fused general path, one launch
+// per world step, no sweep buffer; else the sweep starts go to P.sweep for
+// k_gen_toi.
+template <class C, bool TOI>
 __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __restrict__ state, int64_t N, int64_t e,
                                                 bool valid, int s, float* rec_lds, int slot)
 {
     using SS = SolveShape<C>;
     using TW = StateWords<C>;
-    constexpr int G = SS::G, AM = C::AM, NS = C::NS, NAA = C::NAA;
+    constexpr int G = SS::G, AM = C::AM, NS = C::NS, NAA = C::NAA, KC = C::KC;
     const float dt = (float)(1.0 / 60.0);
     const float m = P.inv_mass, Ii = P.inv_I;
     const Cont<C, ContGlbStore<C>> K{{state, N, e, P.w_cont}};
@@ -187,7 +346,26 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
     const int sc = s < NS ? s : NS - 1;
     StaticG g;
     V2 lo, hi;
-    group_static<C>(P, state, N, e, valid && s < NS && s >= kNumWalls, sc, g, lo, hi);
+    float bhx, bhy;
+    int bmeta;
+    group_static<C>(P, state, N, e, valid && s < NS && s >= kNumWalls, sc, g, lo, hi, bhx, bhy, bmeta);
+    // the stored impulses of this lane's contacts that were touching
+    // (agent-static pairs (i, s); agent pair p = s), fetched with the state:
+    // Collide only zeroes contacts that leave the list, so these are the
+    // values the velocity constraints start from
+    float pni[AM], pti[AM], pan = 0.0f, pat = 0.0f;
+#pragma unroll
+    for (int i = 0; i < AM; ++i) {
+        pni[i] = pti[i] = 0.0f;
+        if (valid && s < NS && bit(ast0[i], s)) {
+            pni[i] = K.asni(i, s);
+            pti[i] = K.asti(i, s);
+        }
+    }
+    if (valid && s < NAA && bit(aat0, s)) {
+        pan = K.aani(s);
+        pat = K.aati(s);
+    }
     const float inv_dt = 1.0f / dt;
     const float dtRatio = inv_dt0 * dt;
     MAS_PROF(P, kPfLoad);
@@ -325,7 +503,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             for (int j = i + 1; j < AM; ++j)
                 if (aa_index<AM>(i, j) == s) { pi = i; pj = j; }
         const bool reset = bit(aa_eval, s) && !bit(aat0, s);
-        const float sni = reset ? 0.0f : K.aani(s), sti = reset ? 0.0f : K.aati(s);
+        const float sni = reset ? 0.0f : pan, sti = reset ? 0.0f : pat;
         VC k = vc_init_aa(sel(c, pi), sel(c, pj), P.agent_r, m, Ii, m, Ii);
         k.ni = dtRatio * sni;
         k.ti = dtRatio * sti;
@@ -346,7 +524,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             collide_pc(g.poly, g.p, g.q, c[i], kPolyRadius, P.agent_r, ln, lp);
             VC k = vc_init_as(g.p, g.q, ln, lp, c[i], P.agent_r, m, Ii);
             const bool reset = bit(my_new, i);
-            const float sni = reset ? 0.0f : K.asni(i, s), sti = reset ? 0.0f : K.asti(i, s);
+            const float sni = reset ? 0.0f : pni[i], sti = reset ? 0.0f : pti[i];
             k.ni = dtRatio * sni;
             k.ti = dtRatio * sti;
             const int q = before[i] + __popc(ast[i] & ((1u << s) - 1u));
@@ -376,6 +554,23 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             key = __float_as_int(R.at(kRkey, q));
             return sel(label, slot_i(key)) == r;
         };
+        // the island's contacts (canonical order) into KC register slots;
+        // more than KC (rare) keeps them in LDS (the loops below)
+        int qi[KC];
+        int nqi = 0;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) qi[j] = 0;
+#pragma unroll 1
+        for (int q = 0; q < nq; ++q) {
+            int key;
+            if (!mine(q, key)) continue;
+#pragma unroll
+            for (int j = 0; j < KC; ++j) qi[j] = opq(j == nqi ? q : qi[j]);
+            ++nqi;
+        }
+        if (nqi <= KC) {
+            island_solve_regs<C>(P, R, K, qi, nqi, members, c, a, v, w, sl, dt, new_awake);
+        } else {
         auto load_vc = [&](int q) {
             VC k;
             k.normal = mk(R.at(kRnx, q), R.at(kRny, q));
@@ -526,18 +721,87 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
                 w[j] = 0.0f;
             }
         }
-        // the island's bodies (b2Island::Solve writes back every member)
+        }  // more than KC island contacts
+        if (!TOI) {
+            // the island's bodies (b2Island::Solve writes back every member)
 #pragma unroll
-        for (int j = 0; j < AM; ++j) {
-            if (!bit(members, j)) continue;
-            const float out[7] = {c[j].x, c[j].y, a[j], v[j].x, v[j].y, w[j], sl[j]};
+            for (int j = 0; j < AM; ++j) {
+                if (!bit(members, j)) continue;
+                const float out[7] = {c[j].x, c[j].y, a[j], v[j].x, v[j].y, w[j], sl[j]};
 #pragma unroll
-            for (int q = 0; q < 7; ++q) state[state_index(7 * j + q, e, N)] = __float_as_uint(out[q]);
+                for (int q = 0; q < 7; ++q) state[state_index(7 * j + q, e, N)] = __float_as_uint(out[q]);
+            }
         }
     }
     MAS_PROF(P, kPfSolve);
     const uint32_t awake_fin = (awake_pre & ~solved) | group_or<G>(new_awake);
+    uint32_t toi_ran = 0;
+    if (TOI) {
+        // every lane takes the solved bodies from its island's root lane
+        const int base = (int)(threadIdx.x & 63) & ~(G - 1);
+#pragma unroll
+        for (int j = 0; j < AM; ++j) {
+            if (!bit(solved, j)) continue;
+            const int src = base + label[j];
+            c[j] = mk(__shfl(c[j].x, src, 64), __shfl(c[j].y, src, 64));
+            a[j] = __shfl(a[j], src, 64);
+            v[j] = mk(__shfl(v[j].x, src, 64), __shfl(v[j].y, src, 64));
+            w[j] = __shfl(w[j], src, 64);
+            sl[j] = __shfl(sl[j], src, 64);
+        }
+        // the island solve's impulse stores are ordered before SolveTOI's
+        // impulse resets (the same words, other lanes of this wave)
+        __threadfence_block();
+        MAS_PROF(P, kPfSolve);
+        // ---------------- b2World::SolveTOI, agent by agent on the group ----------------
+        // (TOI events of different agents are independent: statics never
+        // move, agent-agent pairs are not TOI pairs.)  An agent whose sweep
+        // every static's conservative pre-test rejects has no event and
+        // SolveTOI changes nothing for it (toi_agent_group's first pass):
+        // skipped.
+#pragma unroll
+        for (int i = 0; i < AM; ++i) {
+            const bool act = valid && bit(alive, i) && bit(awake_fin, i);
+            const bool keep = act && s < ns && !toi_reject(g, cs[i], c[i], P.agent_r);
+            if (group_ballot<G>(keep) == 0u) continue;
+            EnvL<C> L;
+            L.alive_m = alive;
+            L.awake_m = awake_fin;
+            L.nbox = nbox;
+#pragma unroll
+            for (int k = 0; k < AM; ++k) {
+                L.c[k] = c[i];
+                L.a[k] = a[i];
+                L.v[k] = v[i];
+                L.w[k] = w[i];
+            }
+#pragma unroll
+            for (int k = 0; k < C::BM; ++k) {
+                L.bp[k] = g.p;
+                L.bhx[k] = bhx;
+                L.bhy[k] = bhy;
+                L.bmeta[k] = bmeta;
+            }
+            const ToiGroupOut o = toi_agent_group<C, G>(L, P, K, i, s, cs[i], as_[i], ast[i], dt);
+            c[i] = o.c;
+            a[i] = o.a;
+            v[i] = o.v;
+            w[i] = o.w;
+            const uint32_t keepm = ~((ns >= 32) ? 0xffffffffu : ((1u << ns) - 1u));
+            ast[i] = (ast[i] & keepm) | o.touch;
+            toi_ran |= 1u << i;
+            if (P.toi_diag && o.events && s == 0 && valid) atomicAdd(P.toi_diag + e, o.events);
+        }
+        MAS_PROF(P, kPfToi);
+    }
     if (!valid) return;
+    if (TOI && s < AM && ((solved | toi_ran) >> s & 1u)) {
+        // agent s's body after the island solve and its SolveTOI
+        const V2 cc = sel(c, s), vv = sel(v, s);
+        const float out[7] = {cc.x, cc.y, sel(a, s), vv.x, vv.y, sel(w, s), sel(sl, s)};
+#pragma unroll
+        for (int q = 0; q < 7; ++q) state[state_index(7 * s + q, e, N)] = __float_as_uint(out[q]);
+    }
     // touching words, awake mask, b2World's previous 1/dt, the sweep starts
     if (s == 0) {
         if (aat != aat0) K.set_aat(aat);
@@ -549,7 +813,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
     }
     // agents woken by Collide that no island holds cannot exist (a woken agent
     // is alive and awake, so its island is solved); the sweep of agent s
-    if (s < AM) {
+    if (!TOI && s < AM) {
         float* sw = P.sweep + e * (3 * AM) + 3 * s;
         const V2 c0s = sel(cs, s);
         sw[0] = c0s.x;

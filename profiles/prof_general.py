@@ -17,7 +17,9 @@ import torch  # noqa: E402
 
 from masurvival import abi  # noqa: E402
 
-SOLVE = {0: 'solve: state + contact load', 1: 'solve: collide', 2: 'solve: island solve', 4: 'solve: store'}
+SOLVE = {0: 'solve: state + contact load', 1: 'solve: collide', 2: 'solve: island solve', 3: 'solve: SolveTOI (fused)',
+         4: 'solve: store'}
+EPW = 8  # envs per wave of k_gen_solve_g for the 2v2 class (64 / SolveShape::G)
 TOI = {20: 'toi: load + sweep', 21: 'toi: reject pre-tests', 22: 'toi: b2TimeOfImpact', 24: 'toi: TOI events',
        23: 'toi: min / exit'}
 
@@ -63,7 +65,7 @@ def main():
 
 def report(buf, gen_envs, steps):
     g = gen_envs / steps
-    ws, wt = 2 * (g + 63) // 64, 2 * (4 * g + 63) // 64  # active waves per step (2 world steps)
+    ws, wt = 2 * (g + EPW - 1) // EPW, 2 * (4 * g + 63) // 64  # active waves per step (2 world steps)
     print(f'# general-path envs per step {g:.0f}; active waves per step: solve {ws:.0f}, toi {wt:.0f}')
     for tab, w in ((SOLVE, ws), (TOI, wt)):
         tot = 0.0
