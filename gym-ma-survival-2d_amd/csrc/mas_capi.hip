@@ -39,6 +39,9 @@ MAS_DECLARE(2v2)
 #ifdef MAS_HAVE_ffa
 MAS_DECLARE(ffa)
 #endif
+#ifdef MAS_HAVE_ffal
+MAS_DECLARE(ffal)
+#endif
 #ifdef MAS_HAVE_xl
 MAS_DECLARE(xl)
 #endif
@@ -502,6 +505,9 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
 #endif
 #ifdef MAS_HAVE_ffa
     if (!ok && fits(4, 16, 16, 4)) { h->ops = Ops{class_info_ffa(), launch_step_ffa, launch_reset_ffa, launch_view_ffa}; ok = true; }
+#endif
+#ifdef MAS_HAVE_ffal
+    if (!ok && fits(4, 24, 16, 8)) { h->ops = Ops{class_info_ffal(), launch_step_ffal, launch_reset_ffal, launch_view_ffal}; ok = true; }
 #endif
 #ifdef MAS_HAVE_xl
     if (!ok && fits(8, 8, 8, 4)) { h->ops = Ops{class_info_xl(), launch_step_xl, launch_reset_xl, launch_view_xl}; ok = true; }
