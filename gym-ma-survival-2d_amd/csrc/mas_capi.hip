@@ -532,7 +532,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 8) * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 8) * sizeof(int));
     h->sweep = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * 8 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * kToiListAgents * sizeof(float));
     h->P.sweep = h->sweep;
     h->gen_flag = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->gen_flag, (size_t)n_envs);
@@ -547,8 +547,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.force_general = 0;
     h->P.solve_one_lane = 0;
     h->toi = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->toi, ((size_t)2 * n_envs * 8 + 2) * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->toi, 0, ((size_t)2 * n_envs * 8 + 2) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h->toi, ((size_t)2 * n_envs * kToiListAgents + 2) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->toi, 0, ((size_t)2 * n_envs * kToiListAgents + 2) * sizeof(int));
     h->P.toi_count = h->toi;
     h->P.toi_list = h->toi ? h->toi + 2 : nullptr;
     h->P.toi_diag = nullptr;

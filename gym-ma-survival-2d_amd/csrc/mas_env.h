@@ -31,6 +31,7 @@ constexpr int kNumWalls = 4;
 constexpr int kMaxPhases = 9;   // zone radii incl. the appended 0
 constexpr int kStats = 19;      // MAS_STATS_WIDTH
 constexpr int kMaxLasers = 32;  // MAS_MAX_LASERS
+constexpr int kToiListAgents = 8;  // agents per env the SolveTOI (env, agent) list is sized for (mas_create)
 
 template <int AM_, int HM_, int BM_, int SM_, int KC_>
 struct Cap {
@@ -115,6 +116,19 @@ __device__ __forceinline__ void prof_mark(const Params& P, int k)
 #define MAS_PROF(P, k) ((void)0)
 #endif
 enum ProfPhase { kPfLoad, kPfCollide, kPfSolve, kPfToi, kPfStore, kPfCount };
+
+// LDS ordering inside a one-wave workgroup (every env kernel's workgroup is
+// one wave): a wave's DS instructions execute in program order, so only the
+// compiler must not move LDS accesses across this point (AMDGPU memory model:
+// wavefront-scope fences emit nothing).  __syncthreads would also wait for
+// the wave's outstanding global stores (s_waitcnt vmcnt(0)) -- in k_obs's
+// column-window loop, each window's tile stores.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ---------------------------------------------------------------------------
 // select helpers for runtime indices into register arrays

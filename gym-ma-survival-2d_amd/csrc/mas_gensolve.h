@@ -46,7 +46,9 @@ struct SolveShape {
     static constexpr int G = need <= 8 ? 8 : (need <= 16 ? 16 : 32);  // lanes per env
     static constexpr int EPW = kWG / G;                               // envs per wave
     static constexpr int KL = C::NAA + C::AM * C::NS;                 // contact records per env
+    static constexpr int KR = C::KC < 4 ? C::KC : 4;                  // island contacts held in registers
     static_assert(need <= 32, "one lane per static / agent pair, 32-bit group ballots");
+    static_assert(C::AM <= kToiListAgents, "the sweep buffer holds kToiListAgents agents per env (mas_create)");
 };
 
 // contact record fields in LDS ([field][q][env of the wave])
@@ -147,11 +149,11 @@ __device__ __forceinline__ void group_static(const Params& P, const uint32_t* __
 // world_solve, mas_physics.h).  new_awake: the members still awake.
 template <class C, class KT>
 __device__ __forceinline__ void island_solve_regs(const Params& P, const SolveRec<C>& R, const KT& K,
-                                                  const int (&qi)[C::KC], int n, uint32_t members, V2 (&c)[C::AM],
+                                                  const int (&qi)[SolveShape<C>::KR], int n, uint32_t members, V2 (&c)[C::AM],
                                                   float (&a)[C::AM], V2 (&v)[C::AM], float (&w)[C::AM],
                                                   float (&sl)[C::AM], float dt, uint32_t& new_awake)
 {
-    constexpr int KC = C::KC, AM = C::AM;
+    constexpr int KC = SolveShape<C>::KR, AM = C::AM;
     const float m = P.inv_mass, Ii = P.inv_I;
     VC k[KC];
     int key[KC];
@@ -301,7 +303,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
 {
     using SS = SolveShape<C>;
     using TW = StateWords<C>;
-    constexpr int G = SS::G, AM = C::AM, NS = C::NS, NAA = C::NAA, KC = C::KC;
+    constexpr int G = SS::G, AM = C::AM, NS = C::NS, NAA = C::NAA, KC = SS::KR;
     const float dt = (float)(1.0 / 60.0);
     const float m = P.inv_mass, Ii = P.inv_I;
     const Cont<C, ContGlbStore<C>> K{{state, N, e, P.w_cont}};
@@ -539,7 +541,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             R.at(kRppx, q) = pp.x; R.at(kRppy, q) = pp.y;
         }
     }
-    __syncthreads();  // the records are in LDS (the workgroup is this wave)
+    wave_lds_sync();  // the records are in LDS (the workgroup is this wave)
 
     // ---------------- b2Island::Solve of the island agent s roots ----------------
     uint32_t new_awake = 0;  // this root's members' awake bits after sleep
@@ -554,8 +556,8 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             key = __float_as_int(R.at(kRkey, q));
             return sel(label, slot_i(key)) == r;
         };
-        // the island's contacts (canonical order) into KC register slots;
-        // more than KC (rare) keeps them in LDS (the loops below)
+        // the island's contacts (canonical order) into KR (<= 4) register
+        // slots; more (rare) keeps them in LDS (the loops below)
         int qi[KC];
         int nqi = 0;
 #pragma unroll

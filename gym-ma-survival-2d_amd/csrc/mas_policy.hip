@@ -28,6 +28,7 @@
 //                writes h1, h2, dA1, dA2, dz feature-major ([F][M] bf16) for
 //                the weight-gradient GEMMs and per-block loss partials.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <cstdint>
 
@@ -1180,7 +1181,10 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     A.da2 = (__bf16*)da2;
     A.dz = (__bf16*)dz;
     A.partials = partials;
-    const bool o32 = ld <= pol::kOff32Ld;
+    // MAS_POL_FORCE_OFF64=1 (test hook, read per call): the 64-bit store
+    // offsets that only buffers over 4 GB take, on any size
+    const char* f64 = getenv("MAS_POL_FORCE_OFF64");
+    const bool o32 = ld <= pol::kOff32Ld && !(f64 && f64[0] == '1');
     auto k = A.ks1 == 10 ? (o32 ? pol::k_policy_train<10, true> : pol::k_policy_train<10, false>)
              : A.ks1 == 9 ? (o32 ? pol::k_policy_train<9, true> : pol::k_policy_train<9, false>)
                           : (o32 ? pol::k_policy_train<0, true> : pol::k_policy_train<0, false>);

@@ -448,7 +448,7 @@ __device__ __forceinline__ void update_seen_dealt(const EnvL<C>& L, const Params
             ++p;
         }
     }
-    __syncthreads();  // the list and the fixture tables / zeroed seen rows are visible
+    wave_lds_sync();  // the list and the fixture tables / zeroed seen rows are visible (one-wave block)
     const float eps1 = (float)(1.0 + 1e-6);
     for (int t = lane; t < total; t += 64) {
         const uint32_t en = list[t];
@@ -461,7 +461,7 @@ __device__ __forceinline__ void update_seen_dealt(const EnvL<C>& L, const Params
         const V2 end = add(pos, scl(eps1, d));
         if (ray_cast_fixtab(P, To, pos, end) == body) atomicOr(&scr.seen[body * S + col], 1u << pc);
     }
-    __syncthreads();
+    wave_lds_sync();  // the LDS seen rows are complete (one-wave block)
 }
 
 // update_seen for the single camera slot `cam` (k_cameras runs one lane per
@@ -523,7 +523,7 @@ __device__ __forceinline__ void update_seen_cam(const EnvL<C>& L, const Params& 
         cand &= cand - 1;
         list[at++] = ((uint32_t)p << 16) | ((uint32_t)lane << 8) | (uint32_t)body;
     }
-    __syncthreads();  // the block is this wave: the list and every fixture table are visible
+    wave_lds_sync();  // the block is this wave: the list and every fixture table are visible
     constexpr int S = kWG / C::AM;
     const float eps1 = (float)(1.0 + 1e-6);
     for (int j = lane; j < total; j += 64) {
@@ -537,7 +537,7 @@ __device__ __forceinline__ void update_seen_cam(const EnvL<C>& L, const Params& 
         const V2 end = add(opos, scl(eps1, d));
         if (ray_cast_fixtab(P, To, opos, end) == body) atomicOr(&seen[body * S + o / C::AM], 1u << pc);
     }
-    __syncthreads();
+    wave_lds_sync();  // the LDS seen rows are complete (one-wave block)
 }
 
 // Cameras.seen <-> state bytes (kGSeen): byte k = camera-position mask of body k
@@ -1183,12 +1183,12 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
                 rj->y2[at] = e.y;
                 ++at;
             }
-            __syncthreads();  // the block is this wave: the job list and the fixture tables are visible
+            wave_lds_sync();  // the block is this wave: the job list and the fixture tables are visible
             for (int j = lane; j < total; j += 64) {
                 const FixTab<C> To{T.f, (int)(rj->who[j] >> 8)};
                 rj->hit[j] = (int16_t)ray_cast_fixtab(P, To, mk(rj->x1[j], rj->y1[j]), mk(rj->x2[j], rj->y2[j]));
             }
-            __syncthreads();
+            wave_lds_sync();
             at = first;
 #pragma unroll
             for (int i = 0; i < C::AM; ++i) {

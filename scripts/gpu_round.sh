@@ -56,6 +56,8 @@ for step in "$@"; do
         python3 $R/bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/prof_ffa.log 2>&1 || exit $?
       cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_1v1 -o run -- \
         python3 $R/bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline > $O/prof_1v1.log 2>&1 || exit $? ;;
+    profk)
+      cd $R && timeout -k 10 300 python -u profiles/prof_kernels.py 65536 20 > $O/prof_kernels.log 2>&1 || exit $? ;;
     profgen)
       cd $R && timeout -k 10 300 python -u profiles/prof_toi.py 65536 4 > $O/prof_toi.log 2>&1 || exit $?
       cd $R && timeout -k 10 300 python -u profiles/prof_general.py 65536 20 --ppo > $O/prof_general.log 2>&1 || exit $? ;;

@@ -98,8 +98,12 @@ def _cos(a, b):
     return float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
 
 
-@pytest.mark.parametrize('D,M', [(160, 8192), (138, 2000 + 7)])
-def test_policy_train_gradients_match_reference(D, M):
+@pytest.mark.parametrize('D,M,off64', [(160, 8192, False), (138, 2000 + 7, False), (160, 8192, True)])
+def test_policy_train_gradients_match_reference(D, M, off64, monkeypatch):
+    # off64: the 64-bit store-offset instantiation of k_policy_train, which only
+    # activation buffers over 4 GB select (mas_policy.hip, MAS_POL_FORCE_OFF64)
+    if off64:
+        monkeypatch.setenv('MAS_POL_FORCE_OFF64', '1')
     p = _policy(D, seed=D + 1)
     cfg = PPOConfig()
     fp = FusedPolicy(p, D, torch.device('cuda'))
