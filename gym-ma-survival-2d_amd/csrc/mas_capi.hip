@@ -56,7 +56,11 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
 hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, int64_t xb_stride, const int8_t* act,
                         const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
                         float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
-                        int64_t ld, float* partials, hipStream_t s);
+                        int64_t ld, float* partials, hipStream_t s, bool rm);
+int policy_rm_feature(int col);
+int64_t policy_adam_scratch();
+hipError_t policy_adam(int64_t n, float* p, const float* g, float* m, float* v, float grad_scale, float max_norm,
+                       double lr, double b1, double b2, double eps, int64_t step, float* scratch, hipStream_t s);
 int64_t policy_dw_scratch(int F, int G, int64_t K);
 hipError_t policy_dw(int F, int G, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* out,
                      float* scratch, hipStream_t s);
@@ -822,7 +826,7 @@ int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const 
     if (!policy_x_ok(obs_dim, x_stride) || (reinterpret_cast<uintptr_t>(x_bf16) & 15))
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_train: x must be 16-B aligned with a padded row stride");
     HIP_TRY(policy_train(packed, obs_dim, n_rows, x_bf16, x_stride, actions, old_logp, adv, ret, clip, vf_coef,
-                         ent_coef, scale, h1, h2, da1, da2, dz, n_rows, partials, (hipStream_t)stream));
+                         ent_coef, scale, h1, h2, da1, da2, dz, n_rows, partials, (hipStream_t)stream, false));
     return MAS_OK;
 }
 
@@ -837,7 +841,41 @@ int mas_policy_train_ld(const void* packed, int32_t obs_dim, int64_t n_rows, con
     if (!policy_x_ok(obs_dim, x_stride) || (reinterpret_cast<uintptr_t>(x_bf16) & 15))
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_train_ld: x must be 16-B aligned with a padded row stride");
     HIP_TRY(policy_train(packed, obs_dim, n_rows, x_bf16, x_stride, actions, old_logp, adv, ret, clip, vf_coef,
-                         ent_coef, scale, h1, h2, da1, da2, dz, ld, partials, (hipStream_t)stream));
+                         ent_coef, scale, h1, h2, da1, da2, dz, ld, partials, (hipStream_t)stream, false));
+    return MAS_OK;
+}
+
+int mas_policy_train_rm(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
+                        const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
+                        float vf_coef, float ent_coef, float scale, void* h1, void* h2, int64_t ld_h, void* da1,
+                        void* da2, void* dz, float* partials, void* stream)
+{
+    const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (!packed || obs_dim <= 0 || n_rows <= 0 || !x_bf16 || !actions || !old_logp || !adv || !ret || !h1 || !h2 ||
+        !da1 || !da2 || !dz || !partials || ld_h < 257 || (ld_h % 8) != 0)
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_train_rm: bad argument (ld_h >= 257, a multiple of 8)");
+    if (!al16(h1) || !al16(h2) || !al16(da1) || !al16(da2) || !al16(dz))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_train_rm: activation buffers must be 16-B aligned");
+    if (!policy_x_ok(obs_dim, x_stride) || !al16(x_bf16))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_train_rm: x must be 16-B aligned with a padded row stride");
+    HIP_TRY(policy_train(packed, obs_dim, n_rows, x_bf16, x_stride, actions, old_logp, adv, ret, clip, vf_coef,
+                         ent_coef, scale, h1, h2, da1, da2, dz, ld_h, partials, (hipStream_t)stream, true));
+    return MAS_OK;
+}
+
+int32_t mas_policy_rm_feature(int32_t col) { return col >= 0 && col < 256 ? policy_rm_feature(col) : -1; }
+
+int64_t mas_policy_adam_scratch(void) { return policy_adam_scratch(); }
+
+int mas_policy_adam(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float grad_scale,
+                    float max_norm, double lr, double beta1, double beta2, double eps, int64_t step, float* scratch,
+                    void* stream)
+{
+    if (n <= 0 || !params || !grads || !exp_avg || !exp_avg_sq || !scratch || step < 1 || !(lr >= 0.0f) ||
+        !(beta1 >= 0.0f && beta1 < 1.0f) || !(beta2 >= 0.0f && beta2 < 1.0f) || !(eps >= 0.0f))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_adam: bad argument (n > 0, step >= 1, 0 <= beta < 1)");
+    HIP_TRY(policy_adam(n, params, grads, exp_avg, exp_avg_sq, grad_scale, max_norm, lr, beta1, beta2, eps, step,
+                        scratch, (hipStream_t)stream));
     return MAS_OK;
 }
 

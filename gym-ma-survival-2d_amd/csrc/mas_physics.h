@@ -1920,13 +1920,32 @@ __device__ __forceinline__ bool world_step_fast(EnvL<C>& L, const Params& P, flo
             L.w[i] = 0.0f;
         }
     }
-    // SolveTOI: every sweep of an awake agent must be rejected by the cheap test
+    // SolveTOI: every sweep of an awake agent must be rejected by the cheap test.
+    // World-AABB pre-filter first (changes no result): a sweep whose box, grown
+    // by sqrt(2) R plus a rounding margin, misses the static's world AABB lies
+    // outside toi_reject's grown local rectangle under any rotation of the
+    // static, so toi_reject would return true; it runs only for the statics
+    // this filter keeps (agents near a wall or a box).
+    const float Rp =
+        1.4143f * ((kPolyRadius + P.agent_r - 3.0f * kLinearSlop) + 0.25f * kLinearSlop + 0.02f) + 0.05f;
 #pragma unroll
     for (int i = 0; i < C::AM; ++i) {
         if (!(bit(L.alive_m, i) && bit(L.awake_m, i))) continue;
+        const V2 slo = mk(fminf(c0[i].x, L.c[i].x) - Rp, fminf(c0[i].y, L.c[i].y) - Rp);
+        const V2 shi = mk(fmaxf(c0[i].x, L.c[i].x) + Rp, fmaxf(c0[i].y, L.c[i].y) + Rp);
 #pragma unroll
         for (int s = 0; s < C::NS; ++s) {
             if (s >= ns) continue;
+            V2 lo, hi;
+            if (s < kNumWalls) {
+                lo = P.wall_lo[s];
+                hi = P.wall_hi[s];
+            } else {
+                const int b = s - kNumWalls;
+                lo = mk(L.bp[b].x - L.bhx[b], L.bp[b].y - L.bhy[b]);
+                hi = mk(L.bp[b].x + L.bhx[b], L.bp[b].y + L.bhy[b]);
+            }
+            if (slo.x > hi.x || shi.x < lo.x || slo.y > hi.y || shi.y < lo.y) continue;
             StaticG g = static_geom(L, P, s);
             if (!toi_reject(g, c0[i], L.c[i], P.agent_r)) bail = true;
         }

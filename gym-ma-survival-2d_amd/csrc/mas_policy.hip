@@ -28,6 +28,7 @@
 //                writes h1, h2, dA1, dA2, dz feature-major ([F][M] bf16) for
 //                the weight-gradient GEMMs and per-block loss partials.
 #include <hip/hip_runtime.h>
+#include <cmath>
 #include <cstdlib>
 
 #include <cstdint>
@@ -41,6 +42,7 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 constexpr int kH = 256;   // hidden width
 constexpr int kMT = 8;    // 32-row M-tiles of a hidden layer
 constexpr int kO = 16;    // real outputs of layer 3 (15 logits + value)
+constexpr float kTanhC = 2.8853900817779268f;  // 2 log2(e)
 #ifndef MAS_POL_WAVES
 #define MAS_POL_WAVES 4
 #endif
@@ -69,7 +71,7 @@ struct Layout {
     __host__ __device__ int64_t w23() const { return w1() + (int64_t)ks1 * kMT * 64; }
     __host__ __device__ int64_t wbk() const { return w23() + 2 * kHalf * 64; }
     __host__ __device__ int64_t nfrag() const { return wbk() + (kBk0 + 2 * kBk1) * 64; }
-    // biases (floats) after the fragments: b1p [8][2][16], b2p [8][2][16], b3 [16]
+    // biases (floats) after the fragments: b1p [8][2][16], b2p [8][2][16] (both x kTanhC), b3 [16]
     __host__ __device__ int64_t b1() const { return nfrag() * 4; }
     __host__ __device__ int64_t b2() const { return b1() + kMT * 2 * 16; }
     __host__ __device__ int64_t b3() const { return b2() + kMT * 2 * 16; }
@@ -141,7 +143,8 @@ __global__ void k_pack(int D, int ks1, const float* __restrict__ W1, const float
         const int rem = (int)(u % (kMT * 2 * 16));
         const int mt = rem / 32, h = (rem / 16) & 1, i = rem & 15;
         const float* b = which == 0 ? b1 : b2;
-        fb[(which == 0 ? L.b1() : L.b2()) + rem] = b[32 * mt + crow(i, h)];
+        // hidden biases pre-scaled for tanh_pre (2 log2(e) b)
+        fb[(which == 0 ? L.b1() : L.b2()) + rem] = b[32 * mt + crow(i, h)] * kTanhC;
     } else if (u < 2 * kMT * 2 * 16 + kO) {
         const int o = (int)(u - 2 * kMT * 2 * 16);
         fb[L.b3() + o] = b3[o];
@@ -172,15 +175,19 @@ __device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c)
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// tanh(x) = (e - 1) / (e + 1), e = 2^(2 x log2(e)): one v_exp_f32 and one
-// v_rcp_f32 (~1 ulp each; the result is rounded to bf16 anyway)
-__device__ __forceinline__ float tanh_fast(float x)
+// tanh(a + b) from the pre-scaled bias bc = kTanhC b (the packed image holds
+// it): 1 - 2 / (2^(kTanhC (a + b)) + 1), five instructions -- FMA, v_exp_f32,
+// add, v_rcp_f32, FMA -- where (e - 1) / (e + 1) after a clamp took eight.
+// No clamp needed: 2^(+large) = inf gives 1, 2^(-large) = 0 gives -1
+// (~1 ulp each for exp / rcp; the result is rounded to bf16 anyway).
+__device__ __forceinline__ float tanh_pre(float a, float bc)
 {
-    if (MAS_POL_EXP & 1) return x;
-    x = fminf(fmaxf(x, -15.0f), 15.0f);
-    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
-    return (e - 1.0f) * __builtin_amdgcn_rcpf(e + 1.0f);
+    if (MAS_POL_EXP & 1) return a;
+    const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(a, kTanhC, bc));
+    return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
+// tanh'(z) = 1 - h^2 from the stored activation h
+__device__ __forceinline__ float dtanh(float h) { return __builtin_fmaf(-h, h, 1.0f); }
 
 __device__ __forceinline__ float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ float log_fast(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
@@ -346,7 +353,7 @@ __device__ __forceinline__ void tanh_h1(const f16v (&acc)[kMT], const float* __r
         float b[16];
         load16(b1p + (mt * 2 + h) * 16, b);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) h1[mt][i >> 3][i & 7] = (__bf16)tanh_fast(acc[mt][i] + b[i]);
+        for (int i = 0; i < 16; ++i) h1[mt][i >> 3][i & 7] = (__bf16)tanh_pre(acc[mt][i], b[i]);
     }
 }
 
@@ -429,7 +436,7 @@ __device__ __forceinline__ f16v layers23(STG& S, const bf8* __restrict__ W23,
             load16(b2p + (mo * 2 + h) * 16, b);
             bf8 f[2];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) f[i >> 3][i & 7] = (__bf16)tanh_fast(a[i] + b[i]);
+            for (int i = 0; i < 16; ++i) f[i >> 3][i & 7] = (__bf16)tanh_pre(a[i], b[i]);
             const bf8* w3 = wl + (kMT / 2 * 16 + 2 * q) * 64 + l;
             z3 = mfma(w3[0], f[0], z3);
             z3 = mfma(w3[64], f[1], z3);
@@ -562,8 +569,9 @@ struct TrainArgs {
     const float* adv;       // [M] (normalised)
     const float* ret;       // [M]
     float clip, vf_coef, ent_coef, scale;  // scale = 1 / rows of the minibatch
-    __bf16 *h1, *h2, *da1, *da2, *dz;      // feature-major [256 | 16][ld]
-    int64_t ld;             // their row stride (>= M; a power of two costs HBM bandwidth)
+    __bf16 *h1, *h2, *da1, *da2, *dz;      // feature-major [256 | 16][ld], or row-major (RM)
+    int64_t ld;             // feature-major: their row stride (>= M; a power of two costs HBM bandwidth);
+                            // RM: the row stride of h1 / h2 (>= 257: column 256 holds the ones)
     float* partials;        // [gridDim.x][4]: sum pg, sum (v-ret)^2, sum entropy, clipped count
 };
 
@@ -647,7 +655,25 @@ __device__ __forceinline__ void store_rows4(__bf16* base, int64_t M, int64_t row
     }
 }
 
-template <int KS, bool OFF32>
+// Row-major activation store (RM): lane (row, h) writes its M-tile fragment as
+// two 16-B chunks of its own row, at columns 32 mt + 8 h (registers 0..7) and
+// 32 mt + 16 + 8 h (registers 8..15).  No lane exchange: stored column
+// 32 mt + 16 c + 8 h + j holds feature 32 mt + crow(8 c + j, h) (rm_feature);
+// the weight-gradient GEMMs sum over rows, so the host un-permutes their
+// [256 x G] results instead of the activations.
+__host__ __device__ inline int rm_feature(int col)
+{
+    const int t = col & 31;
+    return (col & ~31) + crow(8 * (t >> 4) + (t & 7), (t >> 3) & 1);
+}
+__device__ __forceinline__ void store_rm(__bf16* base, int64_t ldr, int64_t row, int mt, int h, const bf8 (&v)[2])
+{
+    bf8* p = reinterpret_cast<bf8*>(base + row * ldr + 32 * mt + 8 * h);
+    p[0] = v[0];
+    p[2] = v[1];
+}
+
+template <int KS, bool OFF32, bool RM>
 __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_policy_train(TrainArgs A)
 {
     const Layout Lo{A.ks1};
@@ -688,11 +714,12 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
         const int rows_per_lane = !MAS_POL_PAIR ? 1 : ((M | LD) & 3) == 0 ? MAS_POL_PAIR : ((M | LD) & 1) == 0 ? 2 : 1;
         const bool pair = rows_per_lane > 1;
         auto store_rows = [&](__bf16* base, int t, const bf8 (&v)[2]) {
-            if (rows_per_lane == 4) store_rows4(base, LD, row, t, h, v);
+            if (RM) store_rm(base, base == A.h1 || base == A.h2 ? LD : kH, row, t, h, v);
+            else if (rows_per_lane == 4) store_rows4(base, LD, row, t, h, v);
             else store_rows2<OFF32>(base, LD, row, t, h, v);
         };
         if (on && ok) {
-            if (pair) {
+            if (RM || pair) {
 #pragma unroll
                 for (int mt = 0; mt < kMT; ++mt) {
                     store_rows(A.h1, mt, h1[mt]);
@@ -769,12 +796,19 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
             st[1] = dv * dv;
             st[2] = ent;
             st[3] = fabsf(ratio - 1.0f) > A.clip ? 1.0f : 0.0f;
+            if (!RM) {
 #pragma unroll
-            for (int o = 0; o < kO; ++o) A.dz[(int64_t)o * LD + row] = (__bf16)dz[o];
+                for (int o = 0; o < kO; ++o) A.dz[(int64_t)o * LD + row] = (__bf16)dz[o];
+            }
         }
         bf8 dzf[2];
 #pragma unroll
         for (int i = 0; i < 16; ++i) dzf[i >> 3][i & 7] = (__bf16)dz[i];
+        if (RM && on && h == 0 && ok) {  // dz row-major [M][16], natural output order
+            bf8* pz = reinterpret_cast<bf8*>(A.dz + row * kO);
+            pz[0] = dzf[0];
+            pz[1] = dzf[1];
+        }
         // dA2 = (W3^T dz) * (1 - h2^2), by M-tile of layer 2
         bf8 da2[kMT][2];
         const bf8* W3T = wb + l;
@@ -786,10 +820,10 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const float hv = (float)h2[mo][i >> 3][i & 7];
-                da2[mo][i >> 3][i & 7] = (__bf16)(g[i] * (1.0f - hv * hv));
+                da2[mo][i >> 3][i & 7] = (__bf16)(g[i] * dtanh(hv));
             }
             if (ok) {
-                if (pair) {
+                if (RM || pair) {
                     store_rows(A.da2, mo, da2[mo]);
                 } else {
 #pragma unroll
@@ -811,9 +845,9 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const float hv = (float)h1[mt][i >> 3][i & 7];
-                    d1[i >> 3][i & 7] = (__bf16)(g[i] * (1.0f - hv * hv));
+                    d1[i >> 3][i & 7] = (__bf16)(g[i] * dtanh(hv));
                 }
-                if (pair) {
+                if (RM || pair) {
                     store_rows(A.da1, mt, d1);
                 } else {
 #pragma unroll
@@ -1140,6 +1174,78 @@ hipError_t policy_pack(int D, const float* W1, const float* b1, const float* W2,
     return hipGetLastError();
 }
 
+int policy_rm_feature(int col) { return pol::rm_feature(col); }
+
+// ---------------------------------------------------------------------------
+// The PPO optimizer step over the policy's flat fp32 parameters (the trainer
+// keeps parameters, gradients and both Adam moments as views into four flat
+// buffers): torch.nn.utils.clip_grad_norm_ followed by torch.optim.Adam (no
+// weight decay, no amsgrad) as two launches -- a split sum of squares, then
+// every block re-sums the partials and updates its share -- instead of the
+// ~20 foreach / norm / copy launches of the torch step per minibatch.
+namespace pol {
+constexpr int kAdamBlocks = 128;  // partial sums of the gradient norm
+__device__ __forceinline__ float block_sum256(float v, float* red)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ __launch_bounds__(256) void k_adam_sqsum(int64_t n, const float* __restrict__ g, float scale,
+                                                    float* __restrict__ part)
+{
+    __shared__ float red[4];
+    float s = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float x = g[i] * scale;
+        s += x * x;
+    }
+    s = block_sum256(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+__global__ __launch_bounds__(256) void k_adam_update(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                                     float* __restrict__ m, float* __restrict__ v,
+                                                     const float* __restrict__ part, float scale, float max_norm,
+                                                     float b2, float w1, float w2, float step_size, float sqrt_bc2,
+                                                     float eps)
+{
+    __shared__ float red[4];
+    const float s = block_sum256(threadIdx.x < kAdamBlocks ? part[threadIdx.x] : 0.0f, red);
+    // clip_grad_norm_: coef = max_norm / (norm + 1e-6), clamped to 1 (applied even when it is 1)
+    const float coef = max_norm > 0.0f ? fminf(max_norm / (sqrtf(s) + 1e-6f), 1.0f) : 1.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float gi = (g[i] * scale) * coef;
+        float mi = m[i];
+        mi = mi + w1 * (gi - mi);                     // exp_avg.lerp_(grad, w1 = 1 - beta1)
+        const float vi = v[i] * b2 + w2 * (gi * gi);  // exp_avg_sq.mul_(beta2).addcmul_(g, g, w2 = 1 - beta2)
+        const float den = sqrtf(vi) / sqrt_bc2 + eps;
+        p[i] = p[i] + (-step_size) * (mi / den);
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+}  // namespace pol
+
+int64_t policy_adam_scratch() { return pol::kAdamBlocks; }
+
+hipError_t policy_adam(int64_t n, float* p, const float* g, float* m, float* v, float grad_scale, float max_norm,
+                       double lr, double b1, double b2, double eps, int64_t step, float* scratch, hipStream_t s)
+{
+    // torch.optim.Adam's scalars are Python floats (double) rounded once to
+    // float by the foreach kernels: the bias corrections, lr / bc1, and the
+    // lerp / addcmul weights 1 - beta (1 - 0.999f in float would be 1.3e-5 off)
+    const double bc1 = 1.0 - std::pow(b1, (double)step), bc2 = 1.0 - std::pow(b2, (double)step);
+    const float step_size = (float)(lr / bc1), sqrt_bc2 = (float)std::sqrt(bc2);
+    hipLaunchKernelGGL(pol::k_adam_sqsum, dim3(pol::kAdamBlocks), dim3(256), 0, s, n, g, grad_scale, scratch);
+    const int64_t nb = (n + 255) / 256 < 512 ? (n + 255) / 256 : 512;
+    hipLaunchKernelGGL(pol::k_adam_update, dim3((unsigned)nb), dim3(256), 0, s, n, p, g, m, v, scratch, grad_scale,
+                       max_norm, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), step_size, sqrt_bc2, (float)eps);
+    return hipGetLastError();
+}
+
+
 // workgroups of the train kernel (= its partial records) and of the act kernel
 int64_t policy_blocks(int64_t M) { return (M + 32 * pol::kTWaves - 1) / (32 * pol::kTWaves); }
 static int64_t act_blocks(int64_t M) { return (M + 32 * pol::kWaves - 1) / (32 * pol::kWaves); }
@@ -1158,7 +1264,7 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
 hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, int64_t xb_stride, const int8_t* act,
                         const float* old_logp, const float* adv, const float* ret, float clip, float vf_coef,
                         float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
-                        int64_t ld, float* partials, hipStream_t s)
+                        int64_t ld, float* partials, hipStream_t s, bool rm)
 {
     pol::TrainArgs A;
     A.ld = ld;
@@ -1185,9 +1291,11 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     // offsets that only buffers over 4 GB take, on any size
     const char* f64 = getenv("MAS_POL_FORCE_OFF64");
     const bool o32 = ld <= pol::kOff32Ld && !(f64 && f64[0] == '1');
-    auto k = A.ks1 == 10 ? (o32 ? pol::k_policy_train<10, true> : pol::k_policy_train<10, false>)
-             : A.ks1 == 9 ? (o32 ? pol::k_policy_train<9, true> : pol::k_policy_train<9, false>)
-                          : (o32 ? pol::k_policy_train<0, true> : pol::k_policy_train<0, false>);
+    auto k = rm ? (A.ks1 == 10 ? pol::k_policy_train<10, false, true>
+                   : A.ks1 == 9 ? pol::k_policy_train<9, false, true> : pol::k_policy_train<0, false, true>)
+           : A.ks1 == 10 ? (o32 ? pol::k_policy_train<10, true, false> : pol::k_policy_train<10, false, false>)
+           : A.ks1 == 9 ? (o32 ? pol::k_policy_train<9, true, false> : pol::k_policy_train<9, false, false>)
+                        : (o32 ? pol::k_policy_train<0, true, false> : pol::k_policy_train<0, false, false>);
     hipLaunchKernelGGL(k, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kTWaves), 0, s, A);
     return hipGetLastError();
 }

@@ -1273,7 +1273,7 @@ __device__ __forceinline__ void compact_cont_row(const KT& K, int i, uint32_t ke
 // pending groups changed.  KT: contact-memory accessor (despawn compaction
 // shifts the agent-static contact rows).
 template <class C, class KT>
-__device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT& K)
+__device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT& K, bool cont_owner = true)
 {
     bool changed = false;
     {
@@ -1298,7 +1298,8 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
             for (int b = 0; b < C::BM; ++b)
                 if (b < L.nbox && L.bhealth[b] > 0) kept |= 1u << b;
 #pragma unroll 1
-            for (int i = 0; i < C::AM; ++i) compact_cont_row<C>(K, i, kept, L.nbox);
+            for (int i = 0; i < C::AM; ++i)
+                if (cont_owner) compact_cont_row<C>(K, i, kept, L.nbox);
             // stable compaction; dead boxes queue (pos, copy_shape(proto), cause)
             int wi = 0;
 #pragma unroll
@@ -1329,6 +1330,9 @@ __device__ __forceinline__ bool box_health(EnvL<C>& L, const Params& P, const KT
     }
     return changed;
 }
+
+// (cont_owner: this lane moves the HBM contact rows; k_cameras runs
+// box_health on every camera lane of an env, the first one owning them)
 
 // agents: Cameras.post_step over the pre-despawn list runs between step_phys
 // and step_post (k_cameras); step_post reads and compacts its bytes.

@@ -84,6 +84,13 @@ SIGNATURES = {
     'mas_policy_train_ld': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                       c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
                             + [c_void_p] * 5 + [c_int64, c_void_p, c_void_p]),
+    'mas_policy_train_rm': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+                            + [c_void_p, c_void_p, c_int64] + [c_void_p] * 5),
+    'mas_policy_rm_feature': (c_int32, [c_int32]),
+    'mas_policy_adam_scratch': (c_int64, []),
+    'mas_policy_adam': (c_int32, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
+                                  c_double, c_double, c_double, c_double, c_int64, c_void_p, c_void_p]),
     'mas_policy_dw_scratch': (c_int64, [c_int32, c_int32, c_int64]),
     'mas_policy_dw': (c_int32, [c_int32, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                 c_void_p]),

@@ -222,6 +222,14 @@ _DW_LAYERS = os.environ.get('MAS_POL_DW', '23')
 # MAS_ACT_PAD: extra columns of the feature-major activation buffers (row
 # stride M + pad; 0 = the power-of-two stride: dW2 kernel 1.21 vs 0.85 ms)
 _ACT_PAD = int(os.environ.get('MAS_ACT_PAD', '64'))
+# MAS_POL_LAYOUT: activation layout of the update ('fm' feature-major
+# [F][rows] with the DPP row pairing and the mas_policy_dw kernels, 'rm'
+# row-major [rows][F] written as plain 16-B stores, weight gradients as
+# row-sum GEMMs)
+_POL_LAYOUT = os.environ.get('MAS_POL_LAYOUT', 'fm')
+_RM_LDH = 264  # row stride of the row-major h1 / h2 (column 256: ones)
+# MAS_FUSED_ADAM=0: the torch clip_grad_norm_ + Adam step in the fused trainer
+_FUSED_ADAM = os.environ.get('MAS_FUSED_ADAM', '1') != '0'
 
 
 def _splitk_nt(a, b):
@@ -232,6 +240,16 @@ def _splitk_nt(a, b):
     c = _split_k(K)
     pa = a.unflatten(1, (c, K // c)).permute(1, 0, 2)
     pb = b.unflatten(1, (c, K // c)).permute(1, 2, 0)
+    return torch.bmm(pa, pb).sum(0, dtype=torch.float32)
+
+
+def _splitk_tn(a, b):
+    """a [K, F]^T @ b [K, G] in fp32 for a huge K (both row-major, any row
+    stride): the row-sum GEMM of the row-major activations."""
+    K = a.shape[0]
+    c = _split_k(K)
+    pa = a.unflatten(0, (c, K // c)).transpose(1, 2)
+    pb = b.unflatten(0, (c, K // c))
     return torch.bmm(pa, pb).sum(0, dtype=torch.float32)
 
 
@@ -259,6 +277,13 @@ class FusedPolicy:
         self.packed = torch.empty((int(self.lib.mas_policy_packed_bytes(self.D)),), dtype=torch.uint8, device=device)
         self._bufs = None
         self._dwbuf = {}
+        self.layout = _POL_LAYOUT
+        if self.layout == 'rm':
+            perm = [int(self.lib.mas_policy_rm_feature(c)) for c in range(256)]  # stored column -> feature
+            q = [0] * 256
+            for c, f in enumerate(perm):
+                q[f] = c
+            self._rm_q = torch.tensor(q, dtype=torch.long, device=device)  # feature -> stored column
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -291,6 +316,46 @@ class FusedPolicy:
                                            ctypes.c_void_p(obs.data_ptr()), xp, self.Dx, int(seed), int(step),
                                            ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(logp.data_ptr()),
                                            ctypes.c_void_p(value.data_ptr()), self._stream()))
+
+    def _buffers_rm(self, M):
+        if self._bufs is None or self._bufs['M'] != M:
+            bf = dict(dtype=torch.bfloat16, device=self.device)
+            nb = int(self.lib.mas_policy_blocks(M))
+            h1 = torch.zeros((M, _RM_LDH), **bf)
+            h2 = torch.zeros((M, _RM_LDH), **bf)
+            h1[:, 256] = 1.0
+            h2[:, 256] = 1.0
+            self._bufs = {'M': M, 'h1': h1, 'h2': h2, 'da1': torch.empty((M, 256), **bf),
+                          'da2': torch.empty((M, 256), **bf), 'dz': torch.empty((M, 16), **bf),
+                          'part': torch.empty((nb, 4), dtype=torch.float32, device=self.device)}
+        return self._bufs
+
+    def _grads_rm(self, xb, actions, old_logp, adv, ret, cfg):
+        M = xb.shape[0]
+        B = self._buffers_rm(M)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        check(self.lib.mas_policy_train_rm(ptr(self.packed), self.D, M, ptr(xb), self.Dx, ptr(actions),
+                                           ptr(old_logp), ptr(adv), ptr(ret), cfg.clip, cfg.vf_coef, cfg.ent_coef,
+                                           1.0 / M, ptr(B['h1']), ptr(B['h2']), _RM_LDH, ptr(B['da1']),
+                                           ptr(B['da2']), ptr(B['dz']), ptr(B['part']), self._stream()))
+        q = self._rm_q
+        g3 = _splitk_tn(B['dz'], B['h2'][:, :257])               # [16, 257], columns stored order
+        g2 = _splitk_tn(B['da2'], B['h1'][:, :257])              # [256, 257]
+        g1 = _splitk_tn(B['da1'], xb[:, :self.D + 1])            # [256, D + 1]
+        g2 = g2.index_select(0, q)
+        p = self.policy
+        l1, l2, l3 = p.body[0], p.body[2], p.head
+        grads = {l3.weight: g3[:, :256].index_select(1, q), l3.bias: g3[:, 256],
+                 l2.weight: g2[:, :256].index_select(1, q), l2.bias: g2[:, 256],
+                 l1.weight: g1.index_select(0, q)[:, :self.D], l1.bias: g1[:, self.D].index_select(0, q)}
+        for prm, g in grads.items():
+            if prm.grad is None:
+                prm.grad = g.to(prm.dtype).clone(memory_format=torch.contiguous_format)
+            else:
+                prm.grad.copy_(g)
+        s = B['part'].sum(0) / M
+        pg, v, ent, clipfrac = s[0], s[1], s[2], s[3]
+        return pg + cfg.vf_coef * v - cfg.ent_coef * ent, pg, v, ent, clipfrac
 
     def _buffers(self, M):
         if self._bufs is None or self._bufs['M'] != M:
@@ -329,6 +394,8 @@ class FusedPolicy:
         assert xb.dtype == torch.bfloat16 and xb.shape[1] == self.Dx and xb.is_contiguous()
         for t in (actions, old_logp, adv, ret):
             assert t.is_contiguous()
+        if self.layout == 'rm':
+            return self._grads_rm(xb, actions, old_logp, adv, ret, cfg)
         B = self._buffers(M)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         check(self.lib.mas_policy_train_ld(ptr(self.packed), self.D, M, ptr(xb), self.Dx, ptr(actions),
@@ -373,6 +440,61 @@ def policy_loss_reference(policy, x, actions, old_logp, adv, ret, cfg: 'PPOConfi
     pg = -torch.min(ratio * adv, ratio.clamp(1 - cfg.clip, 1 + cfg.clip) * adv).mean()
     vl = F.mse_loss(v, ret)
     return pg + cfg.vf_coef * vl - cfg.ent_coef * ent.mean(), pg, vl, ent.mean()
+
+
+class FusedAdam:
+    """clip_grad_norm_ + torch.optim.Adam.step() for the fused trainer as one
+    HIP launch pair (include/masurvival.h mas_policy_adam).  The parameters,
+    their gradients and both Adam moments become views into four flat fp32
+    buffers; the torch.optim.Adam object keeps holding them as its state, so
+    its state_dict (checkpoints) is unchanged.  bind_state() re-points that
+    state after Adam.load_state_dict replaced it."""
+
+    def __init__(self, params, opt: torch.optim.Adam, lib, device):
+        self.params, self.opt, self.lib, self.device = list(params), opt, lib, device
+        n = sum(p.numel() for p in self.params)
+        f = dict(dtype=torch.float32, device=device)
+        self.p, self.g = torch.empty((n,), **f), torch.zeros((n,), **f)
+        self.m, self.v = torch.zeros((n,), **f), torch.zeros((n,), **f)
+        self.scratch = torch.empty((int(lib.mas_policy_adam_scratch()),), **f)
+        self.spans = []
+        off = 0
+        with torch.no_grad():
+            for prm in self.params:
+                k = prm.numel()
+                self.p[off:off + k].copy_(prm.detach().reshape(-1))
+                prm.data = self.p[off:off + k].view_as(prm)
+                prm.grad = self.g[off:off + k].view_as(prm)
+                self.spans.append((off, k))
+                off += k
+        self.bind_state()
+
+    @torch.no_grad()
+    def bind_state(self):
+        for prm, (off, k) in zip(self.params, self.spans):
+            st = self.opt.state[prm]
+            if 'exp_avg' in st:
+                self.m[off:off + k].copy_(st['exp_avg'].reshape(-1))
+                self.v[off:off + k].copy_(st['exp_avg_sq'].reshape(-1))
+            else:
+                self.m[off:off + k].zero_()
+                self.v[off:off + k].zero_()
+                st['step'] = torch.tensor(0.0)
+            st['exp_avg'] = self.m[off:off + k].view_as(prm)
+            st['exp_avg_sq'] = self.v[off:off + k].view_as(prm)
+
+    def step(self, max_norm: float, grad_scale: float = 1.0):
+        grp = self.opt.param_groups[0]
+        steps = [self.opt.state[prm]['step'] for prm in self.params]
+        for t in steps:
+            t += 1  # CPU scalars, as torch.optim.Adam keeps them
+        b1, b2 = grp['betas']
+        check(self.lib.mas_policy_adam(self.p.numel(), ctypes.c_void_p(self.p.data_ptr()),
+                                       ctypes.c_void_p(self.g.data_ptr()), ctypes.c_void_p(self.m.data_ptr()),
+                                       ctypes.c_void_p(self.v.data_ptr()), float(grad_scale), float(max_norm),
+                                       float(grp['lr']), float(b1), float(b2), float(grp['eps']),
+                                       int(steps[0].item()), ctypes.c_void_p(self.scratch.data_ptr()),
+                                       ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
 
 
 class RolloutBuffer:
@@ -441,6 +563,7 @@ class PPOTrainer:
         if fused is None:
             fused = self.device.type == 'cuda' and cfg.hidden == 256
         self.fused = None
+        self.fused_opt = None
         if fused:
             self.fused = FusedPolicy(self.policy, env.obs_dim, self.device)
             b = self.buf
@@ -449,6 +572,8 @@ class PPOTrainer:
             self._boot = (torch.empty((M, 6), dtype=torch.int8, device=self.device),
                           torch.empty((M,), dtype=torch.float32, device=self.device))
             self.fused.pack()
+            if _FUSED_ADAM and not any(g.get('weight_decay', 0) or g.get('amsgrad') for g in self.opt.param_groups):
+                self.fused_opt = FusedAdam(self.policy.parameters(), self.opt, self.fused.lib, self.device)
         else:
             self._sync_rollout_policy()
 
@@ -537,10 +662,16 @@ class PPOTrainer:
                 M = xb.shape[0]
                 loss, pg, vl, ent, cf = self.fused.grads(xb, b.actions[sl].reshape(M, 6), b.logp[sl].reshape(M),
                                                          b.adv[sl].reshape(M), b.ret[sl].reshape(M), c)
-                if self.collectives:
-                    _allreduce_grads(params, self.world, self.group)
-                nn.utils.clip_grad_norm_(params, c.max_grad_norm)
-                self.opt.step()
+                if self.fused_opt is not None:
+                    # flat gradient buffer: one all-reduce, the 1 / world folded into the step
+                    if self.collectives:
+                        dist.all_reduce(self.fused_opt.g, group=self.group)
+                    self.fused_opt.step(c.max_grad_norm, 1.0 / self.world if self.collectives else 1.0)
+                else:
+                    if self.collectives:
+                        _allreduce_grads(params, self.world, self.group)
+                    nn.utils.clip_grad_norm_(params, c.max_grad_norm)
+                    self.opt.step()
                 self.fused.pack()
         self.last_stats = {'loss': loss.detach(), 'pg': pg.detach(), 'v': vl.detach(), 'entropy': ent.detach(),
                            'clipfrac': cf.detach()}
@@ -602,6 +733,8 @@ class PPOTrainer:
     def load_state_dict(self, sd):
         self.policy.load_state_dict(sd['policy'])
         self.opt.load_state_dict(sd['opt'])
+        if self.fused_opt is not None:
+            self.fused_opt.bind_state()
         self.steps_taken = int(sd['steps_taken'])
         self.seed = int(sd['seed'])
         self.gen.set_state(sd['gen'].cpu())  # generator states are CPU ByteTensors (map_location moves them)

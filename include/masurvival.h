@@ -241,6 +241,33 @@ int mas_policy_train_ld(const void* packed, int32_t obs_dim, int64_t n_rows, con
                         const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
                         float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,
                         int64_t ld, float* partials, void* stream);
+/* mas_policy_train_rm: the same kernel writing the activations ROW-major,
+ * each lane storing its own row as 16-B chunks (no lane exchange):
+ * h1, h2 [n_rows][ld_h] (ld_h >= 257, a multiple of 8; the caller keeps
+ * column 256 = 1, the bias column, the kernel writes columns 0..255),
+ * dA1, dA2 [n_rows][256], dz [n_rows][16] (outputs in natural order).
+ * Within every 32-column tile the 256 hidden columns are stored permuted:
+ * column c holds hidden feature mas_policy_rm_feature(c).  The weight
+ * gradients are then the row-sum GEMMs dW2 = dA2^T h1, dW3 = dz^T h2,
+ * dW1 = dA1^T x with rows / columns mapped back through that permutation. */
+int mas_policy_train_rm(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
+                        const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
+                        float vf_coef, float ent_coef, float scale, void* h1, void* h2, int64_t ld_h, void* da1,
+                        void* da2, void* dz, float* partials, void* stream);
+int32_t mas_policy_rm_feature(int32_t col);
+
+/* mas_policy_adam: one PPO optimizer step over flat fp32 buffers of n
+ * parameters, replacing torch.nn.utils.clip_grad_norm_(params, max_norm)
+ * followed by torch.optim.Adam.step() (no weight decay, no amsgrad):
+ * g' = grad_scale * grads (1 / world size after a summing all-reduce),
+ * scaled by min(1, max_norm / (|g'|_2 + 1e-6)) (max_norm <= 0: no clipping),
+ * then exp_avg, exp_avg_sq and params updated in place with the bias
+ * corrections of `step` (>= 1, the step being taken).  grads is not written.
+ * scratch: mas_policy_adam_scratch() floats. */
+int64_t mas_policy_adam_scratch(void);
+int mas_policy_adam(int64_t n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float grad_scale,
+                    float max_norm, double lr, double beta1, double beta2, double eps, int64_t step, float* scratch,
+                    void* stream);
 
 /* mas_policy_dw: the weight and bias gradients of one policy layer from the
  * feature-major activations mas_policy_train writes, over the minibatch rows:

@@ -16,6 +16,7 @@ import pytest
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
+from masurvival import ppo as ppo_mod  # noqa: E402
 from masurvival.ppo import (FusedPolicy, PolicyMLP, PPOConfig, evaluate_actions,  # noqa: E402
                             policy_loss_reference, sample_actions_hip)
 
@@ -98,12 +99,17 @@ def _cos(a, b):
     return float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
 
 
-@pytest.mark.parametrize('D,M,off64', [(160, 8192, False), (138, 2000 + 7, False), (160, 8192, True)])
-def test_policy_train_gradients_match_reference(D, M, off64, monkeypatch):
+@pytest.mark.parametrize('D,M,off64,layout', [(160, 8192, False, 'fm'), (138, 2000 + 7, False, 'fm'),
+                                              (160, 8192, True, 'fm'), (160, 8192, False, 'rm'),
+                                              (138, 2000 + 7, False, 'rm')])
+def test_policy_train_gradients_match_reference(D, M, off64, layout, monkeypatch):
     # off64: the 64-bit store-offset instantiation of k_policy_train, which only
-    # activation buffers over 4 GB select (mas_policy.hip, MAS_POL_FORCE_OFF64)
+    # activation buffers over 4 GB select (mas_policy.hip, MAS_POL_FORCE_OFF64);
+    # layout 'rm': row-major activations (mas_policy_train_rm) and the row-sum
+    # GEMMs with the stored-column permutation undone on the host
     if off64:
         monkeypatch.setenv('MAS_POL_FORCE_OFF64', '1')
+    monkeypatch.setattr(ppo_mod, '_POL_LAYOUT', layout)
     p = _policy(D, seed=D + 1)
     cfg = PPOConfig()
     fp = FusedPolicy(p, D, torch.device('cuda'))
@@ -186,3 +192,42 @@ def test_fused_trainer_iteration_on_env():
     # the stored update input is the bf16 image of the observations the policy saw
     assert torch.equal(b.xb[3].view(b.N, b.A, -1)[..., :b.D], b.obs[3].bfloat16())
     env.close()
+
+
+@pytest.mark.parametrize('max_norm,grad_scale', [(0.5, 1.0), (1e9, 0.5)])
+def test_fused_adam_matches_torch(max_norm, grad_scale):
+    """mas_policy_adam (FusedAdam) against clip_grad_norm_ + torch.optim.Adam
+    over five steps of random gradients: one clipped regime, one unclipped
+    with the all-reduce 1 / world scale.  fp32 in both; the bound covers the
+    different summation order of the norm: |d| <= 1e-6 + 1e-5 |p|."""
+    from masurvival.ppo import FusedAdam
+    p_ref = _policy(160, seed=3)
+    p_fus = _policy(160, seed=3)
+    opt_ref = torch.optim.Adam(p_ref.parameters(), lr=3e-4, eps=1e-5)
+    opt_fus = torch.optim.Adam(p_fus.parameters(), lr=3e-4, eps=1e-5)
+    fa = FusedAdam(p_fus.parameters(), opt_fus, FusedPolicy(p_fus, 160, torch.device('cuda')).lib, torch.device('cuda'))
+    g = torch.Generator(device='cuda').manual_seed(11)
+    for _ in range(5):
+        grads = [torch.randn(q.shape, device='cuda', generator=g) * 0.3 for q in p_ref.parameters()]
+        for q, gr in zip(p_ref.parameters(), grads):
+            q.grad = gr * grad_scale
+        torch.nn.utils.clip_grad_norm_(list(p_ref.parameters()), max_norm)
+        opt_ref.step()
+        for q, gr in zip(p_fus.parameters(), grads):
+            q.grad.copy_(gr)
+        fa.step(max_norm, grad_scale)
+    torch.cuda.synchronize()
+    for (name, a), b in zip(p_fus.named_parameters(), p_ref.parameters()):
+        assert bool(((a - b).abs() <= 1e-6 + 1e-5 * b.abs()).all()), name
+        st_a, st_b = opt_fus.state[a], opt_ref.state[b]
+        assert float(st_a['step']) == float(st_b['step']) == 5.0
+        assert torch.allclose(st_a['exp_avg'], st_b['exp_avg'], rtol=1e-5, atol=1e-7), name
+        assert torch.allclose(st_a['exp_avg_sq'], st_b['exp_avg_sq'], rtol=1e-5, atol=1e-9), name
+    # the optimizer's state_dict round-trips into a fresh FusedAdam
+    sd = opt_fus.state_dict()
+    p2 = _policy(160, seed=4)
+    opt2 = torch.optim.Adam(p2.parameters(), lr=3e-4, eps=1e-5)
+    fa2 = FusedAdam(p2.parameters(), opt2, fa.lib, torch.device('cuda'))
+    opt2.load_state_dict(sd)
+    fa2.bind_state()
+    assert torch.equal(fa2.m, fa.m) and torch.equal(fa2.v, fa.v)
