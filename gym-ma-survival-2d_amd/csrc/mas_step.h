@@ -1046,6 +1046,7 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
             ac[i][k] = x < 0 ? 0 : (x > hi ? hi : x);
         }
     if (bad && valid) atomicAdd(P.bad_actions, 1);
+    MAS_PROF(P, 41);
     // ---------------- pre_step ----------------
     // boxes: Object.pre_step drops last step's queued box items (semantics.py:853-856)
 #pragma unroll
@@ -1073,6 +1074,7 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
         L.w[i] += P.inv_I * cross(sub(L.c[i], L.c[i]), J);
         L.w[i] += P.inv_I * ang;
     }
+    MAS_PROF(P, 42);
     // UseLast (semantics.py:300-309): Heal.use (:646-649) / ObjectItem.use (:830-836)
     int uses_heal = 0, uses_box = 0;
 #pragma unroll
@@ -1092,6 +1094,7 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
                       P.ownership ? it_owner(meta) : kCauseNone);
         }
     }
+    MAS_PROF(P, 43);
     // GiveLast (semantics.py:335-370): nearest body centre within the give radius
     {
         int taker[C::AM];
@@ -1138,6 +1141,7 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
             dirty |= kGRule;
         }
     }
+    MAS_PROF(P, 44);
     // Melee / ContinuousMelee (semantics.py:531-554, 584-610): all rays first.
     // A ray (laser_scan: no side effect) is cast only for an agent whose
     // target the attack loop reads -- attacking and off cooldown; the
@@ -1184,11 +1188,13 @@ __device__ __forceinline__ void step_pre(EnvL<C>& L, const Params& P, const FixT
                 ++at;
             }
             wave_lds_sync();  // the block is this wave: the job list and the fixture tables are visible
+            MAS_PROF(P, 45);
             for (int j = lane; j < total; j += 64) {
                 const FixTab<C> To{T.f, (int)(rj->who[j] >> 8)};
                 rj->hit[j] = (int16_t)ray_cast_fixtab(P, To, mk(rj->x1[j], rj->y1[j]), mk(rj->x2[j], rj->y2[j]));
             }
             wave_lds_sync();
+            MAS_PROF(P, 46);
             at = first;
 #pragma unroll
             for (int i = 0; i < C::AM; ++i) {

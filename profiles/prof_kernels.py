@@ -16,7 +16,9 @@ import torch  # noqa: E402,F401
 
 from masurvival import abi  # noqa: E402
 
-MARKS = {30: 'k_pre: state load', 31: 'k_pre: step_pre (rules, melee rays)', 32: 'k_pre: dirty stores',
+MARKS = {30: 'k_pre: state load', 41: 'k_pre: step_pre queue_actions', 42: 'k_pre: step_pre drops + motors',
+         43: 'k_pre: step_pre UseLast', 44: 'k_pre: step_pre GiveLast', 45: 'k_pre: step_pre melee fixtab + jobs',
+         46: 'k_pre: step_pre melee ray casts', 31: 'k_pre: step_pre melee attacks (rest)', 32: 'k_pre: dirty stores',
          33: 'k_pre: contact-free fast physics', 34: 'k_post: state load', 35: 'k_post: step_post',
          36: 'k_post: stores', 37: 'k_obs: auto-reset', 38: 'k_obs: state load', 39: 'k_obs: row writer (windows)',
          40: 'k_obs: tile stores (windows)'}
