@@ -27,7 +27,7 @@ struct ClassInfo {
 #define MAS_DECLARE(NAME)                                                                                     \
     ClassInfo class_info_##NAME();                                                                          \
     void launch_step_##NAME(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const int8_t*, float*, float*, \
-                            uint8_t*, int);                                                                 \
+                            uint8_t*, int, const StepSplit*);                                               \
     void launch_reset_##NAME(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const uint8_t*, float*); \
     void launch_view_##NAME(hipStream_t, const Params&, const uint32_t*, int64_t, int64_t, float*);
 #ifdef MAS_HAVE_1v1
@@ -296,7 +296,8 @@ __global__ __launch_bounds__(256) void k_sample(int64_t M, const float* __restri
 
 struct Ops {
     ClassInfo info;
-    void (*step)(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const int8_t*, float*, float*, uint8_t*, int);
+    void (*step)(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const int8_t*, float*, float*, uint8_t*, int,
+                 const StepSplit*);
     void (*reset)(dim3, hipStream_t, const Params&, uint32_t*, int64_t, const uint8_t*, float*);
     void (*view)(hipStream_t, const Params&, const uint32_t*, int64_t, int64_t, float*);
 };
@@ -309,11 +310,19 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
-    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count + [1] k_gen queue + [1] last step's count
+    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count + [1] k_gen queue + [1] the other count slot + [1] list guard
     uint8_t* gen_flag;  // [N] env left the fast path this step
     int* toi;           // [2] counts + [2][N * 8] SolveTOI (env, agent) lists (8 >= agents of every class)
     float* sweep;
     mas_obs_layout layout;
+    // the split step (launch_step): side stream + fork / join events, made at
+    // the first mas_step on the handle's device; split = 0 (MAS_SPLIT=0 in the
+    // environment at mas_create, or mas_debug_force_general bit 2) keeps the
+    // one-stream order
+    StepSplit sp;
+    bool sp_made;
+    int split, split_default;
+    int par;  // which of the two list-count slots the next mas_step appends to
 };
 
 static void build_layout(mas_handle* h)
@@ -546,7 +555,13 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
     h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
     h->P.gen_next = h->phys ? h->phys + n_envs + 2 : nullptr;
-    h->P.phys_last = h->phys ? h->phys + n_envs + 3 : nullptr;
+    h->P.phys_prev = h->phys ? h->phys + n_envs + 3 : nullptr;
+    h->par = 0;
+    h->sp_made = false;
+    {
+        const char* v = getenv("MAS_SPLIT");
+        h->split = h->split_default = (v && v[0] == '1') ? 1 : 0;
+    }
     h->P.list_overflow = h->phys ? h->phys + n_envs + 4 : nullptr;
     h->P.force_general = 0;
     h->P.solve_one_lane = 0;
@@ -579,6 +594,11 @@ int mas_destroy(mas_handle* h)
     if (h->sweep) (void)hipFree(h->sweep);
     if (h->toi) (void)hipFree(h->toi);
     if (h->gen_flag) (void)hipFree(h->gen_flag);
+    if (h->sp_made) {
+        (void)hipStreamDestroy(h->sp.side);
+        (void)hipEventDestroy(h->sp.fork);
+        (void)hipEventDestroy(h->sp.join);
+    }
     delete h;
     return MAS_OK;
 }
@@ -631,8 +651,25 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
 {
     if (!h || !actions || !obs || !rewards || !done) return fail(MAS_ERR_INVALID_ARG, "mas_step: null argument");
     dim3 g((unsigned)((h->N + kWG - 1) / kWG));
-    h->ops.step(g, (hipStream_t)stream, h->P, h->state, h->N, actions, obs, rewards, done, auto_reset);
+    if (h->split && !h->sp_made) {
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur));
+        HIP_TRY(hipSetDevice(h->device));
+        hipError_t e = hipStreamCreateWithFlags(&h->sp.side, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.fork, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.join, hipEventDisableTiming);
+        (void)hipSetDevice(cur);
+        HIP_TRY(e);
+        h->sp_made = true;
+    }
+    // the two list-count slots alternate: this step appends to one, and its
+    // k_pre zeroes the other (the previous step's) for the next step
+    Params P = h->P;
+    if (h->par) std::swap(P.phys_count, P.phys_prev);
+    h->ops.step(g, (hipStream_t)stream, P, h->state, h->N, actions, obs, rewards, done, auto_reset,
+                h->split ? &h->sp : nullptr);
     HIP_TRY(hipGetLastError());
+    h->par ^= 1;
     return MAS_OK;
 }
 
@@ -713,7 +750,8 @@ int mas_debug_counters(mas_handle* h, int64_t* host_out)
     if (!h || !host_out) return fail(MAS_ERR_INVALID_ARG, "mas_debug_counters: null argument");
     int c = 0;
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(&c, h->P.phys_last, sizeof(int), hipMemcpyDeviceToHost));
+    // the count slot the last mas_step appended to (kept until the next k_pre)
+    HIP_TRY(hipMemcpy(&c, h->par ? h->P.phys_count : h->P.phys_prev, sizeof(int), hipMemcpyDeviceToHost));
     host_out[0] = c;
     return MAS_OK;
 }
@@ -733,6 +771,7 @@ int mas_debug_force_general(mas_handle* h, int32_t on)
     if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: null handle");
     h->P.force_general = (on & 1) ? 1 : 0;
     h->P.solve_one_lane = (on & 2) ? 1 : 0;
+    h->split = (on & 4) ? 0 : h->split_default;
     return MAS_OK;
 }
 

@@ -83,9 +83,9 @@ struct Params {
     float lid_depth;
     double lid_off[kMaxLasers];
     int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
-    int* phys_count;  // number of them
+    int* phys_count;  // number of them: one of two count slots, alternating per mas_step
+    int* phys_prev;   // the other slot (the previous step's count): k_pre zeroes it for the next step
     int* gen_next;    // k_gen work queue: next chunk of the list (reset by k_post)
-    int* phys_last;   // the list count of the last step (mas_debug_counters; k_post)
     int* list_overflow;  // appends to phys_list / toi_list refused by their bounds (mas_debug_guards; must stay 0)
     int force_general;   // test diagnostics (mas_debug_force_general): every env takes the general physics path
     int solve_one_lane;  // test diagnostics (mas_debug_force_general, on = 2): the one-lane-per-env k_gen_solve
@@ -96,6 +96,14 @@ struct Params {
     int* toi_diag;    // test diagnostics (mas_debug_set_toi_counter): per env, TOI events + 65536 per capped SolveTOI
     int* bad_actions; // env-steps whose actions fell outside MultiDiscrete([3,3,3,2,2,2]) (clamped; mas_invalid_actions)
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
+};
+
+// The split step (launch_step): a second stream of the handle for the general
+// path and the general envs' post phases, forked from and joined back into
+// the caller's stream by two events.  Null: the one-stream order.
+struct StepSplit {
+    hipStream_t side;
+    hipEvent_t fork, join;
 };
 
 // Phase timing for the profiling build (make prof -> libmas_prof.so): lane 0
@@ -112,7 +120,22 @@ __device__ __forceinline__ void prof_mark(const Params& P, int k)
     }
 }
 #define MAS_PROF(P, k) ::mas::prof_mark(P, k)
+// a wave's whole span from t0: its max (P.prof[62]) and a histogram in 10-us
+// buckets (P.prof[48 + min(span / 10 us, 13)])
+__device__ __forceinline__ void prof_span(const Params& P, unsigned long long t0)
+{
+    const unsigned long long d = wall_clock64() - t0;
+    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) {
+        atomicMax(&P.prof[62], d);
+        const unsigned long long b = d / 1000ull;
+        atomicAdd(&P.prof[48 + (b < 13ull ? b : 13ull)], 1ull);
+    }
+}
+#define MAS_PROF_T0(v) const unsigned long long v = wall_clock64()
+#define MAS_PROF_SPAN(P, v) ::mas::prof_span(P, v)
 #else
+#define MAS_PROF_T0(v) ((void)0)
+#define MAS_PROF_SPAN(P, v) ((void)0)
 #define MAS_PROF(P, k) ((void)0)
 #endif
 enum ProfPhase { kPfLoad, kPfCollide, kPfSolve, kPfToi, kPfStore, kPfCount };

@@ -74,6 +74,13 @@ def report(buf, gen_envs, steps):
             tot += t
             print(f'{name:30s} {t:8.2f} us per active wave')
         print(f'{"total":30s} {tot:8.2f}')
+    # k_gen_solve_g wave spans (MAS_PROF_SPAN): histogram in 10-us buckets, max
+    hist = [buf[48 + b] for b in range(14)]
+    if sum(hist):
+        print(f'# k_gen_solve_g wave spans over {steps} steps: max {buf[62] * 0.01:.1f} us')
+        for b, c in enumerate(hist):
+            if c:
+                print(f'  {10 * b:4d}-{10 * b + 10 if b < 13 else "":<4} us {c:8d} waves')
 
 
 if __name__ == '__main__':
