@@ -316,9 +316,9 @@ struct mas_handle {
     float* sweep;
     mas_obs_layout layout;
     // the split step (launch_step): side stream + fork / join events, made at
-    // the first mas_step on the handle's device; split = 0 (MAS_SPLIT=0 in the
-    // environment at mas_create, or mas_debug_force_general bit 2) keeps the
-    // one-stream order
+    // the first mas_step that splits, on the handle's device; split = 1 with
+    // MAS_SPLIT=1 in the environment at mas_create or mas_debug_force_general
+    // bit 2, else the one-stream order (default: the split measured slower)
     StepSplit sp;
     bool sp_made;
     int split, split_default;
@@ -771,7 +771,7 @@ int mas_debug_force_general(mas_handle* h, int32_t on)
     if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: null handle");
     h->P.force_general = (on & 1) ? 1 : 0;
     h->P.solve_one_lane = (on & 2) ? 1 : 0;
-    h->split = (on & 4) ? 0 : h->split_default;
+    h->split = (on & 4) ? 1 : h->split_default;
     return MAS_OK;
 }
 

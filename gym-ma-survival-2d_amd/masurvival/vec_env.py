@@ -183,7 +183,15 @@ class VecMaSurvival:
         """Test diagnostics: every env takes the general physics path (on);
         one_lane_solve: the general path's Collide + Solve runs one lane per
         env (k_gen_solve) instead of on lane groups (k_gen_solve_g)."""
-        check(self._lib.mas_debug_force_general(self._h, int(bool(on)) | (2 if one_lane_solve else 0)))
+        bits = getattr(self, '_dbg_bits', 0) & 4
+        self._dbg_bits = bits | int(bool(on)) | (2 if one_lane_solve else 0)
+        check(self._lib.mas_debug_force_general(self._h, self._dbg_bits))
+
+    def split_step(self, on: bool = True):
+        """Test diagnostics: run mas_step split over two streams (the general
+        path and its envs' post phases on a side stream); same results."""
+        self._dbg_bits = (getattr(self, '_dbg_bits', 0) & 3) | (4 if on else 0)
+        check(self._lib.mas_debug_force_general(self._h, self._dbg_bits))
 
     def invalid_actions(self, reset: bool = True) -> int:
         """Env-steps whose actions were out of range (clamped on device) since

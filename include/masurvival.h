@@ -298,10 +298,11 @@ int mas_debug_guards(mas_handle* h, int64_t* host_out);
  * mas_step through the general physics path (the contact-free fast path
  * gives up for all envs); bit 1 runs the general path's Collide + Solve one
  * lane per env (k_gen_solve) instead of on lane groups (k_gen_solve_g);
- * bit 2 runs mas_step on the caller's stream alone (no side stream for the
- * general path and its envs' post phases; also MAS_SPLIT=0 in the
- * environment at mas_create).  Results are unchanged (every path is exact):
- * A/B and parity tests only. */
+ * bit 2 runs mas_step split over two streams (the general path and its
+ * envs' post phases on a side stream of the handle, the other envs' post
+ * phases on the caller's stream; also MAS_SPLIT=1 in the environment at
+ * mas_create; measured slower, so off by default).  Results are unchanged
+ * (every path is exact): A/B and parity tests only. */
 int mas_debug_force_general(mas_handle* h, int32_t on);
 
 /* Action validation.  The reference asserts action_space.contains(actions)
