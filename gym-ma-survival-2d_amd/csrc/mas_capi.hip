@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -316,12 +317,17 @@ struct mas_handle {
     float* sweep;
     mas_obs_layout layout;
     // the split step (launch_step): side stream + fork / join events, made at
-    // the first mas_step that splits, on the handle's device; split = 1 with
-    // MAS_SPLIT=1 in the environment at mas_create or mas_debug_force_general
-    // bit 2, else the one-stream order (default: the split measured slower)
+    // the first mas_step that splits, on the handle's device.  split: 0 the
+    // one-stream order, 1 every general-path env on the side stream
+    // (measured slower), 2 (default) the slow list only; MAS_SPLIT=0/1/2 in
+    // the environment at mas_create, or mas_debug_force_general bits 2 / 3
     StepSplit sp;
     bool sp_made;
     int split, split_default;
+    int* slow;          // [N] slow list + [2] count slots
+    uint8_t* slow_flag; // [N]
+    int* slow_sig;      // host-mapped signal (P.slow_sig): a step flagged a slow env
+    int slow_hold;      // steps left of the slow split since the last signal
     int par;  // which of the two list-count slots the next mas_step appends to
 };
 
@@ -560,9 +566,30 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->sp_made = false;
     {
         const char* v = getenv("MAS_SPLIT");
-        h->split = h->split_default = (v && v[0] == '1') ? 1 : 0;
+        h->split = h->split_default = (v && v[0] >= '0' && v[0] <= '2') ? v[0] - '0' : 2;
+        const char* k = getenv("MAS_SLOW_K");
+        h->P.slow_k = k ? atoi(k) : 4;  // TOI events of an env's step that make it slow (the cap always does)
     }
     h->P.list_overflow = h->phys ? h->phys + n_envs + 4 : nullptr;
+    h->slow = nullptr;
+    h->slow_flag = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&h->slow, ((size_t)n_envs + 4) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->slow, 0, ((size_t)n_envs + 4) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h->slow_flag, (size_t)n_envs);
+    if (e == hipSuccess) e = hipMemset(h->slow_flag, 0, (size_t)n_envs);
+    h->P.slow_list = h->slow;
+    h->P.slow_count = h->slow ? h->slow + n_envs : nullptr;
+    h->P.slow_prev = h->slow ? h->slow + n_envs + 1 : nullptr;
+    h->P.slow_flag = h->slow_flag;
+    h->slow_sig = nullptr;
+    h->slow_hold = 0;
+    h->P.slow_sig = nullptr;
+    h->P.slow_route = 0;
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->slow_sig, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        *h->slow_sig = 0;
+        e = hipHostGetDevicePointer((void**)&h->P.slow_sig, h->slow_sig, 0);
+    }
     h->P.force_general = 0;
     h->P.solve_one_lane = 0;
     h->toi = nullptr;
@@ -594,6 +621,9 @@ int mas_destroy(mas_handle* h)
     if (h->sweep) (void)hipFree(h->sweep);
     if (h->toi) (void)hipFree(h->toi);
     if (h->gen_flag) (void)hipFree(h->gen_flag);
+    if (h->slow) (void)hipFree(h->slow);
+    if (h->slow_flag) (void)hipFree(h->slow_flag);
+    if (h->slow_sig) (void)hipHostFree(h->slow_sig);
     if (h->sp_made) {
         (void)hipStreamDestroy(h->sp.side);
         (void)hipEventDestroy(h->sp.fork);
@@ -665,9 +695,31 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
     // the two list-count slots alternate: this step appends to one, and its
     // k_pre zeroes the other (the previous step's) for the next step
     Params P = h->P;
-    if (h->par) std::swap(P.phys_count, P.phys_prev);
-    h->ops.step(g, (hipStream_t)stream, P, h->state, h->N, actions, obs, rewards, done, auto_reset,
-                h->split ? &h->sp : nullptr);
+    if (h->par) {
+        std::swap(P.phys_count, P.phys_prev);
+        std::swap(P.slow_count, P.slow_prev);
+    }
+    // the slow split runs while the general kernels keep flagging slow envs
+    // (the signal lags the device by the steps in flight: slow envs persist
+    // for many steps); without any, one stream and no fork / join
+    const StepSplit* sp = nullptr;
+    if (h->split == 1) {
+        h->sp.slow = 0;
+        sp = &h->sp;
+    } else if (h->split == 2) {
+        if (__atomic_load_n(h->slow_sig, __ATOMIC_RELAXED)) {
+            __atomic_store_n(h->slow_sig, 0, __ATOMIC_RELAXED);
+            h->slow_hold = 8;
+        }
+        if (h->slow_hold > 0) {
+            --h->slow_hold;
+            h->sp.slow = 1;
+            sp = &h->sp;
+        }
+    } else {
+        P.slow_k = 0;  // no slow flags, no signal
+    }
+    h->ops.step(g, (hipStream_t)stream, P, h->state, h->N, actions, obs, rewards, done, auto_reset, sp);
     HIP_TRY(hipGetLastError());
     h->par ^= 1;
     return MAS_OK;
@@ -748,11 +800,13 @@ int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards
 int mas_debug_counters(mas_handle* h, int64_t* host_out)
 {
     if (!h || !host_out) return fail(MAS_ERR_INVALID_ARG, "mas_debug_counters: null argument");
-    int c = 0;
+    int c = 0, c2 = 0;
     HIP_TRY(hipDeviceSynchronize());
-    // the count slot the last mas_step appended to (kept until the next k_pre)
+    // the count slots the last mas_step appended to (kept until the next k_pre):
+    // the general-path list and the slow list
     HIP_TRY(hipMemcpy(&c, h->par ? h->P.phys_count : h->P.phys_prev, sizeof(int), hipMemcpyDeviceToHost));
-    host_out[0] = c;
+    HIP_TRY(hipMemcpy(&c2, h->par ? h->P.slow_count : h->P.slow_prev, sizeof(int), hipMemcpyDeviceToHost));
+    host_out[0] = (int64_t)c + c2;
     return MAS_OK;
 }
 
@@ -771,7 +825,7 @@ int mas_debug_force_general(mas_handle* h, int32_t on)
     if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: null handle");
     h->P.force_general = (on & 1) ? 1 : 0;
     h->P.solve_one_lane = (on & 2) ? 1 : 0;
-    h->split = (on & 4) ? 1 : h->split_default;
+    h->split = (on & 8) ? 0 : ((on & 4) ? 1 : h->split_default);
     return MAS_OK;
 }
 

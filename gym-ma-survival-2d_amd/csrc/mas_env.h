@@ -95,6 +95,16 @@ struct Params {
     float* sweep;     // [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
     int* toi_diag;    // test diagnostics (mas_debug_set_toi_counter): per env, TOI events + 65536 per capped SolveTOI
     int* bad_actions; // env-steps whose actions fell outside MultiDiscrete([3,3,3,2,2,2]) (clamped; mas_invalid_actions)
+    // the slow split (launch_step): envs whose last general-path step had a
+    // SolveTOI that hit the sub-step cap, or >= slow_k TOI events, go to
+    // their own list, run on the side stream (k_pre routes, gen_flag 2)
+    int* slow_list;      // [N]
+    int* slow_count;     // its count slot this step (alternating, as phys_count)
+    int* slow_prev;      // the other slot: k_pre zeroes it
+    uint8_t* slow_flag;  // [N] set by k_gen_solve_g, read and cleared by k_pre
+    int slow_k;          // 0: no slow flags
+    int slow_route;      // this step routes the flagged envs to the slow list (the slow split is on)
+    int* slow_sig;       // host-mapped: set to 1 when k_gen_solve_g flags an env (the host turns the split on)
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
 
@@ -104,6 +114,7 @@ struct Params {
 struct StepSplit {
     hipStream_t side;
     hipEvent_t fork, join;
+    int slow;  // 1: only the slow list on the side stream; 0: every general-path env
 };
 
 // Phase timing for the profiling build (make prof -> libmas_prof.so): lane 0

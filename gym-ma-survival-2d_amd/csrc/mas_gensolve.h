@@ -738,6 +738,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
     MAS_PROF(P, kPfSolve);
     const uint32_t awake_fin = (awake_pre & ~solved) | group_or<G>(new_awake);
     uint32_t toi_ran = 0;
+    int toi_events = 0;  // TOI events of the env's agents, + 65536 per capped agent
     if (TOI) {
         // every lane takes the solved bodies from its island's root lane
         const int base = (int)(threadIdx.x & 63) & ~(G - 1);
@@ -785,6 +786,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
                 L.bmeta[k] = bmeta;
             }
             const ToiGroupOut o = toi_agent_group<C, G>(L, P, K, i, s, cs[i], as_[i], ast[i], dt);
+            toi_events += o.events;
             c[i] = o.c;
             a[i] = o.a;
             v[i] = o.v;
@@ -795,6 +797,13 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             if (P.toi_diag && o.events && s == 0 && valid) atomicAdd(P.toi_diag + e, o.events);
         }
         MAS_PROF(P, kPfToi);
+        // a slow env (sub-step cap, or many events) takes the slow list next
+        // step (k_pre); the flag was cleared by this step's k_pre
+        if (valid && s == 0 && P.slow_k > 0 && ((toi_events >> 16) != 0 || (toi_events & 0xffff) >= P.slow_k)) {
+            P.slow_flag[e] = 1;
+            // tell the host (mapped memory; a vector store): it turns the slow split on
+            if (P.slow_sig) __hip_atomic_store(P.slow_sig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     if (!valid) return;
     if (TOI && s < AM && ((solved | toi_ran) >> s & 1u)) {

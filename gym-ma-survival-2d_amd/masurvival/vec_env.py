@@ -183,14 +183,16 @@ class VecMaSurvival:
         """Test diagnostics: every env takes the general physics path (on);
         one_lane_solve: the general path's Collide + Solve runs one lane per
         env (k_gen_solve) instead of on lane groups (k_gen_solve_g)."""
-        bits = getattr(self, '_dbg_bits', 0) & 4
+        bits = getattr(self, '_dbg_bits', 0) & 12
         self._dbg_bits = bits | int(bool(on)) | (2 if one_lane_solve else 0)
         check(self._lib.mas_debug_force_general(self._h, self._dbg_bits))
 
-    def split_step(self, on: bool = True):
-        """Test diagnostics: run mas_step split over two streams (the general
-        path and its envs' post phases on a side stream); same results."""
-        self._dbg_bits = (getattr(self, '_dbg_bits', 0) & 3) | (4 if on else 0)
+    def split_step(self, mode=None):
+        """Test diagnostics: how mas_step uses the side stream (same results):
+        0 the caller's stream alone, 1 every general-path env on the side
+        stream, None the handle's default (the slow split, MAS_SPLIT)."""
+        bits = {0: 8, 1: 4, None: 0}[mode]
+        self._dbg_bits = (getattr(self, '_dbg_bits', 0) & 3) | bits
         check(self._lib.mas_debug_force_general(self._h, self._dbg_bits))
 
     def invalid_actions(self, reset: bool = True) -> int:

@@ -298,11 +298,16 @@ int mas_debug_guards(mas_handle* h, int64_t* host_out);
  * mas_step through the general physics path (the contact-free fast path
  * gives up for all envs); bit 1 runs the general path's Collide + Solve one
  * lane per env (k_gen_solve) instead of on lane groups (k_gen_solve_g);
- * bit 2 runs mas_step split over two streams (the general path and its
- * envs' post phases on a side stream of the handle, the other envs' post
- * phases on the caller's stream; also MAS_SPLIT=1 in the environment at
- * mas_create; measured slower, so off by default).  Results are unchanged
- * (every path is exact): A/B and parity tests only. */
+ * bits 2 and 3 pick how mas_step uses the handle's side stream.  Default
+ * (MAS_SPLIT=2 in the environment at mas_create, or unset): the slow split,
+ * the envs whose last general-path step had a SolveTOI at the sub-step cap
+ * (or >= MAS_SLOW_K, default 4, TOI events) run their general path and post
+ * phases on the side stream while the caller's stream runs the rest; it is
+ * on for 8 steps after the general kernels last flagged such an env (a
+ * host-mapped signal), else mas_step runs on one stream.  Bit 2
+ * (or MAS_SPLIT=1): every general-path env on the side stream.  Bit 3 (or
+ * MAS_SPLIT=0): the caller's stream alone.  Results are unchanged (every path
+ * is exact): A/B and parity tests only. */
 int mas_debug_force_general(mas_handle* h, int32_t on);
 
 /* Action validation.  The reference asserts action_space.contains(actions)

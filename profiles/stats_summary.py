@@ -9,15 +9,21 @@ import sys
 
 
 def step_spans(trace):
+    """k_pre start -> the last end of the step's env kernels (mas::k_*, not
+    the policy's mas::pol::*) before the next k_pre: with the split step the
+    side stream's kernels can end after the caller's k_obs."""
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r['Start_Timestamp']))
-    spans, t0 = [], None
+    spans, t0, t1 = [], None, None
     for r in rows:
         n = r['Kernel_Name']
         if 'mas::k_pre<' in n:
-            t0 = int(r['Start_Timestamp'])
-        elif 'mas::k_obs<' in n and t0 is not None:
-            spans.append((int(r['End_Timestamp']) - t0) / 1e6)
-            t0 = None
+            if t0 is not None and t1 is not None:
+                spans.append((t1 - t0) / 1e6)
+            t0, t1 = int(r['Start_Timestamp']), None
+        elif t0 is not None and 'mas::k_' in n and 'mas::pol::' not in n and 'k_stats' not in n:
+            t1 = max(t1 or 0, int(r['End_Timestamp']))
+    if t0 is not None and t1 is not None:
+        spans.append((t1 - t0) / 1e6)
     return spans
 
 
@@ -34,7 +40,7 @@ def main(path, out, header, steps=None, trace=None, timed=None):
     if trace:
         sp = step_spans(trace)
         k = int(timed)
-        lines.append('# mas_step launch group (k_pre start -> k_obs end): mean %.4f ms over the last %d steps '
+        lines.append('# mas_step launch group (k_pre start -> last env kernel end): mean %.4f ms over the last %d steps '
                      '(the timed region), %.4f ms over all %d steps' % (sum(sp[-k:]) / k, k, sum(sp) / len(sp), len(sp)))
     open(out, 'w').write('\n'.join(lines) + '\n')
 

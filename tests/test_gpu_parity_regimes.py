@@ -97,7 +97,7 @@ def test_ppo_regime_policy_actions_match_oracle():
     for _ in range(iters):
         for t in range(H):
             tr.rollout_step(t)
-            gen_cnt += env.gen_flags(flags)
+            gen_cnt += (env.gen_flags(flags) != 0).to(torch.int32)  # 2: the slow list
         acts.append(tr.buf.actions.cpu().numpy())
         rews.append(tr.buf.rewards.cpu().numpy())
         dones.append(tr.buf.dones.cpu().numpy())

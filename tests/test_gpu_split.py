@@ -1,11 +1,21 @@
-"""The split step (mas_debug_force_general bit 2 / MAS_SPLIT=1: the general
-path and the general envs' k_cameras / k_post / k_obs on a side stream, the
-other envs' on the caller's stream) against the one-stream order: two
-handles on the same seeds and actions must give bit-identical obs, rewards,
-done flags and state images, with auto-reset, in the contact-heavy regime
-(random actions for 150 steps first), and with every env forced onto the
-general path (the list-mode kernels then run every env)."""
-import numpy as np
+"""The split steps against the one-stream order (mas_debug_force_general
+bits 2 / 3, MAS_SPLIT): two handles on the same seeds and actions must give
+bit-identical obs, rewards, done flags and state images, with auto-reset.
+
+- mode 1: every general-path env runs its general path and its k_cameras /
+  k_post / k_obs on the handle's side stream, the other envs' on the
+  caller's stream;
+- the default, the slow split: only the envs whose previous general-path
+  step was slow (a SolveTOI at the sub-step cap, or >= MAS_SLOW_K TOI
+  events) go to the side stream.  MAS_SLOW_K=1 here, so that every env with
+  a TOI event the step before takes the side stream and the slow list is
+  busy at these sizes (the product default, 4, picks the few wedged envs of
+  the PPO regime).
+
+The contact-heavy regime is random actions (plus every env forced onto the
+general path in one case: the list-mode kernels then run every env)."""
+import os
+
 import pytest
 
 torch = pytest.importorskip('torch')
@@ -18,16 +28,21 @@ from masurvival.vec_env import VecMaSurvival  # noqa: E402
 HI = torch.tensor([3, 3, 3, 2, 2, 2])
 
 
-@pytest.mark.parametrize('name,cfg,n,T,forced', [('C3 2v2', C3_CONFIG, 8192, 220, False),
-                                                 ('C5 ffa4', C5_CONFIG, 2048, 200, False),
-                                                 ('C3 2v2 forced', C3_CONFIG, 4096, 40, True)])
-def test_split_step_matches_one_stream(name, cfg, n, T, forced):
+@pytest.mark.parametrize('name,cfg,n,T,mode,forced', [('C3 2v2 slow', C3_CONFIG, 8192, 220, None, False),
+                                                      ('C5 ffa4 slow', C5_CONFIG, 2048, 200, None, False),
+                                                      ('C3 2v2 slow forced', C3_CONFIG, 4096, 60, None, True),
+                                                      ('C3 2v2 all', C3_CONFIG, 8192, 120, 1, False),
+                                                      ('C3 2v2 all forced', C3_CONFIG, 4096, 40, 1, True)])
+def test_split_step_matches_one_stream(name, cfg, n, T, mode, forced, monkeypatch):
+    monkeypatch.setenv('MAS_SLOW_K', '1')
+    monkeypatch.delenv('MAS_SPLIT', raising=False)
     try:
         one = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
         two = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
     except abi.MasError as e:
         pytest.skip(str(e))
-    two.split_step(True)
+    one.split_step(0)
+    two.split_step(mode)
     if forced:
         one.force_general(True)
         two.force_general(True)
@@ -35,7 +50,7 @@ def test_split_step_matches_one_stream(name, cfg, n, T, forced):
     gen = torch.Generator(device=one.device)
     gen.manual_seed(n)
     hi = HI.to(one.device)
-    general = 0
+    general = side = 0
     for t in range(T):
         a = (torch.rand((n, one.n_agents, 6), generator=gen, device=one.device) * hi).to(torch.int8)
         o1, r1, d1, _ = one.step(a)
@@ -47,8 +62,14 @@ def test_split_step_matches_one_stream(name, cfg, n, T, forced):
         g1, g2 = one.debug_counters()['phys_general_envs'], two.debug_counters()['phys_general_envs']
         assert g1 == g2, (name, t)
         general += g1
+        f1, f2 = one.gen_flags(), two.gen_flags()
+        assert not bool((f1 == 2).any()), (name, t)  # no slow list on one stream
+        assert torch.equal(f1 != 0, f2 != 0), (name, t)
+        side += int((f2 == 2).sum())
     assert torch.equal(one.get_state(), two.get_state())
     assert general > 0
+    if mode is None:
+        assert side > 0, name  # the slow list ran
     assert one.debug_guards()['list_overflow'] == 0 and two.debug_guards()['list_overflow'] == 0
     one.close()
     two.close()
