@@ -585,6 +585,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->slow_hold = 0;
     h->P.slow_sig = nullptr;
     h->P.slow_route = 0;
+    h->P.gen_sparse = 0;
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->slow_sig, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) {
         *h->slow_sig = 0;

@@ -105,6 +105,9 @@ struct Params {
     int slow_k;          // 0: no slow flags
     int slow_route;      // this step routes the flagged envs to the slow list (the slow split is on)
     int* slow_sig;       // host-mapped: set to 1 when k_gen_solve_g flags an env (the host turns the split on)
+    int gen_sparse;      // k_gen_solve_g maps list entry p to (block p % grid, slot p / grid): one env per wave
+                         // while the list is shorter than the grid (the slow list: the divergent SolveTOI
+                         // chains of two slow envs in one wave would run one after the other)
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
 
