@@ -297,6 +297,11 @@ __device__ __forceinline__ void island_solve_regs(const Params& P, const SolveRe
 // mas_physics.h: lane s owns static s) -- the fused general path, one launch
 // per world step, no sweep buffer; else the sweep starts go to P.sweep for
 // k_gen_toi.
+// 1 (default): the SolveTOI agent loop runs by rank (each group's k-th TOI
+// agent in round k); 0: by agent index
+#ifndef MAS_TOI_BY_RANK
+#define MAS_TOI_BY_RANK 1
+#endif
 template <class C, bool TOI>
 __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __restrict__ state, int64_t N, int64_t e,
                                                 bool valid, int s, float* rec_lds, int slot)
@@ -762,37 +767,62 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
         // every static's conservative pre-test rejects has no event and
         // SolveTOI changes nothing for it (toi_agent_group's first pass):
         // skipped.
+        // the agents this env's SolveTOI runs (the group agrees on the mask)
+        uint32_t need = 0;
 #pragma unroll
         for (int i = 0; i < AM; ++i) {
             const bool act = valid && bit(alive, i) && bit(awake_fin, i);
             const bool keep = act && s < ns && !toi_reject(g, cs[i], c[i], P.agent_r);
-            if (group_ballot<G>(keep) == 0u) continue;
+            if (group_ballot<G>(keep) != 0u) need |= 1u << i;
+        }
+#if MAS_TOI_BY_RANK
+        // Round k runs each group's k-th such agent (ascending index, the
+        // serial order per env), so a wave runs as many rounds as its busiest
+        // env has TOI agents; by agent index, agent i's round ran whenever
+        // any env of the wave needed agent i (up to AM rounds for one agent
+        // per env).  Agents' SolveTOI are independent (statics never move).
+#pragma unroll 1
+        for (int k = 0; k < AM; ++k) {
+            if (!__any(need != 0u)) break;
+            if (need == 0u) continue;
+            const int i = __builtin_ctz(need);
+            need &= need - 1u;
+            const V2 ci = sel(c, i), vi = sel(v, i);
+            const float ai = sel(a, i), wi = sel(w, i);
+#else
+#pragma unroll
+        for (int i = 0; i < AM; ++i) {
+            if (!bit(need, i)) continue;
+            const V2 ci = c[i], vi = v[i];
+            const float ai = a[i], wi = w[i];
+#endif
             EnvL<C> L;
             L.alive_m = alive;
             L.awake_m = awake_fin;
             L.nbox = nbox;
 #pragma unroll
-            for (int k = 0; k < AM; ++k) {
-                L.c[k] = c[i];
-                L.a[k] = a[i];
-                L.v[k] = v[i];
-                L.w[k] = w[i];
+            for (int k2 = 0; k2 < AM; ++k2) {
+                L.c[k2] = ci;
+                L.a[k2] = ai;
+                L.v[k2] = vi;
+                L.w[k2] = wi;
             }
 #pragma unroll
-            for (int k = 0; k < C::BM; ++k) {
-                L.bp[k] = g.p;
-                L.bhx[k] = bhx;
-                L.bhy[k] = bhy;
-                L.bmeta[k] = bmeta;
+            for (int k2 = 0; k2 < C::BM; ++k2) {
+                L.bp[k2] = g.p;
+                L.bhx[k2] = bhx;
+                L.bhy[k2] = bhy;
+                L.bmeta[k2] = bmeta;
             }
-            const ToiGroupOut o = toi_agent_group<C, G>(L, P, K, i, s, cs[i], as_[i], ast[i], dt);
+            const uint32_t asti = sel(ast, i);
+            const ToiGroupOut o = toi_agent_group<C, G>(L, P, K, i, s, sel(cs, i), sel(as_, i), asti, dt);
             toi_events += o.events;
-            c[i] = o.c;
-            a[i] = o.a;
-            v[i] = o.v;
-            w[i] = o.w;
+            put(c, i, o.c);
+            put(a, i, o.a);
+            put(v, i, o.v);
+            put(w, i, o.w);
             const uint32_t keepm = ~((ns >= 32) ? 0xffffffffu : ((1u << ns) - 1u));
-            ast[i] = (ast[i] & keepm) | o.touch;
+            put(ast, i, (asti & keepm) | o.touch);
             toi_ran |= 1u << i;
             if (P.toi_diag && o.events && s == 0 && valid) atomicAdd(P.toi_diag + e, o.events);
         }
