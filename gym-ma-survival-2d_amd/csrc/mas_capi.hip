@@ -686,7 +686,13 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
         int cur = 0;
         HIP_TRY(hipGetDevice(&cur));
         HIP_TRY(hipSetDevice(h->device));
-        hipError_t e = hipStreamCreateWithFlags(&h->sp.side, hipStreamNonBlocking);
+        // the side stream at the highest priority (MAS_SIDE_PRIO=0: default
+        // priority): its few waves carry the step's longest chain
+        int lo = 0, hi = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        const char* pv = getenv("MAS_SIDE_PRIO");
+        const bool prio = !(pv && pv[0] == '0');
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->sp.side, hipStreamNonBlocking, prio ? hi : lo);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.fork, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.join, hipEventDisableTiming);
         (void)hipSetDevice(cur);
