@@ -14,7 +14,7 @@ bit-identical obs, rewards, done flags and state images, with auto-reset.
 
 The contact-heavy regime is random actions (plus every env forced onto the
 general path in one case: the list-mode kernels then run every env)."""
-import os
+import math
 
 import pytest
 
@@ -26,19 +26,27 @@ from masurvival.config import C3_CONFIG, C5_CONFIG  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 
 HI = torch.tensor([3, 3, 3, 2, 2, 2])
+# the Lidars run after the join, over every env (k_lidar reads the state the
+# side stream wrote)
+LID_2V2 = {'agents': {'n_agents': 4, 'agent_size': 1}, 'teams': {'twoteams': True},
+           'melee': {'range': 2, 'damage': 20, 'cooldown': 40, 'drift': True},
+           'lidars': {'n_lasers': 8, 'fov': 0.5 * math.pi, 'depth': 6}}
 
 
-@pytest.mark.parametrize('name,cfg,n,T,mode,forced', [('C3 2v2 slow', C3_CONFIG, 8192, 220, None, False),
-                                                      ('C5 ffa4 slow', C5_CONFIG, 2048, 200, None, False),
-                                                      ('C3 2v2 slow forced', C3_CONFIG, 4096, 60, None, True),
-                                                      ('C3 2v2 all', C3_CONFIG, 8192, 120, 1, False),
-                                                      ('C3 2v2 all forced', C3_CONFIG, 4096, 40, 1, True)])
-def test_split_step_matches_one_stream(name, cfg, n, T, mode, forced, monkeypatch):
+@pytest.mark.parametrize('name,cfg,n,T,mode,forced,ar', [
+    ('C3 2v2 slow', C3_CONFIG, 8192, 220, None, False, True),
+    ('C5 ffa4 slow', C5_CONFIG, 2048, 200, None, False, True),
+    ('C3 2v2 slow forced', C3_CONFIG, 4096, 60, None, True, True),
+    ('C3 2v2 slow no auto-reset', C3_CONFIG, 4096, 160, None, False, False),
+    ('2v2 lidars slow', LID_2V2, 4096, 160, None, False, True),
+    ('C3 2v2 all', C3_CONFIG, 8192, 120, 1, False, True),
+    ('C3 2v2 all forced', C3_CONFIG, 4096, 40, 1, True, True)])
+def test_split_step_matches_one_stream(name, cfg, n, T, mode, forced, ar, monkeypatch):
     monkeypatch.setenv('MAS_SLOW_K', '1')
     monkeypatch.delenv('MAS_SPLIT', raising=False)
     try:
-        one = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
-        two = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
+        one = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=ar)
+        two = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=ar)
     except abi.MasError as e:
         pytest.skip(str(e))
     one.split_step(0)
