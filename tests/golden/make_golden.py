@@ -145,6 +145,27 @@ def collector_actions(obs, rng, A, teams):
     return tuple(acts)
 
 
+def hoarder_actions(obs, rng, A, teams):
+    """Walk over the nearest heal / box item and keep it: never use, give
+    rarely, attack rarely -- inventories fill past four slots (the ffal
+    capacity class: Inventory with slots > 4, semantics.py:165-245)."""
+    acts = collector_actions(obs, rng, A, teams)
+    out = []
+    for a in acts:
+        a = a.copy()
+        a[3] = int(rng.random() < 0.05)
+        a[5] = int(rng.random() < 0.03)
+        out.append(a)
+    return tuple(out)
+
+
+def max_inventory(env):
+    """Longest inventory list of any agent right now (Inventory.inventories)."""
+    sem = sys.modules['masurvival.semantics']
+    invs = env.simulation.groups['agents'].get(sem.Inventory)
+    return max((len(v) for m in invs for v in m.inventories.values()), default=0)
+
+
 def lidar_obs(env, lidars):
     """The 'lidars' observation key of this build: the
     reference's own Lidars module (simulation.py:357-392) computes the scans;
@@ -188,12 +209,15 @@ def run_episode(mod, name, config, env_seed, act_seed, max_steps, p_script):
     A = env.n_agents
     rng = np.random.default_rng(act_seed)
     obs_l, act_l, rew_l, done_l = [flat0], [], [], []
+    max_inv = 0
     for t in range(max_steps):
         if p_script == -1:  # idle stretches (Box2D sleep): no-op except a random burst every 150 steps
             acts = tuple(np.array([1, 1, 1, 0, 0, 0]) if (t % 150) > 3 else rng.integers(0, [3, 3, 3, 2, 2, 2])
                          for _ in range(A))
         elif p_script == -2:
             acts = collector_actions(obs, rng, A, env.has_teams)
+        elif p_script == -3:
+            acts = hoarder_actions(obs, rng, A, env.has_teams)
         else:
             acts = scripted_actions(obs, rng, A, p_script, env.has_teams)
         obs, rew, done, info = env.step(acts)
@@ -203,6 +227,7 @@ def run_episode(mod, name, config, env_seed, act_seed, max_steps, p_script):
         act_l.append(np.stack(acts).astype(np.int8))
         rew_l.append(np.asarray(rew, dtype=np.float32))
         done_l.append(bool(done))
+        max_inv = max(max_inv, max_inventory(env))
         if done:
             break
     stats = env.flush_stats()
@@ -217,6 +242,7 @@ def run_episode(mod, name, config, env_seed, act_seed, max_steps, p_script):
         rewards=np.stack(rew_l),
         done=np.array(done_l, dtype=np.bool_),
         stats=json.dumps({k: float(v) for k, v in stats.items()}),
+        max_inventory=np.int32(max_inv),
     )
 
 
@@ -285,6 +311,27 @@ EPISODES = [
         'melee': MELEE, 'lidars': {'n_lasers': 16, 'fov': 2.0 * math.pi * 15 / 16, 'depth': 5.5}},
      13, 113, 500, -2),
     ('lidars_1v1_s14', {'melee': MELEE, 'lidars': {'n_lasers': 2, 'fov': 0.3, 'depth': 30}}, 14, 114, 400, 0.6),
+    # the ffal capacity class (more than 16 heals or 4 slots): hoarders fill
+    # inventories past four slots (max_inventory > 4 is asserted by the tests)
+    ('ffal_ffa4_s15', {
+        'agents': {'n_agents': 4, 'agent_size': 1},
+        'spawn_grid': {'grid_size': 6, 'floor_size': 16},
+        'heals': {'reset_spawns': {'n_items': 20, 'item_size': 0.5}, 'heal': {'healing': 50}},
+        'boxes': {'reset_spawns': {'n_boxes': 12, 'box_size': 1}, 'ownership': False,
+                  'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20,
+                  'randomized_shape': {'avg_w': 1.0, 'std_w': 0.5, 'avg_h': 1.0, 'std_h': 0.5}},
+        'inventory': {'slots': 6},
+        'safe_zone': {'phases': 5, 'cooldown': 200, 'damage': 1, 'radiuses': [16, 8, 4, 2], 'centers': 'random'},
+        'melee': MELEE}, 15, 115, 1200, -3),
+    ('ffal_2v2_owned_s16', {
+        'agents': {'n_agents': 4, 'agent_size': 1}, 'teams': {'twoteams': True},
+        'spawn_grid': {'grid_size': 7, 'floor_size': 18},
+        'heals': {'reset_spawns': {'n_items': 24, 'item_size': 0.5}, 'heal': {'healing': 50}},
+        'boxes': {'reset_spawns': {'n_boxes': 16, 'box_size': 1}, 'ownership': True,
+                  'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20},
+        'inventory': {'slots': 8},
+        'safe_zone': {'phases': 5, 'cooldown': 200, 'damage': 1, 'radiuses': [16, 8, 4, 2], 'centers': 'random'},
+        'melee': MELEE}, 16, 116, 1200, -3),
 ]
 
 
@@ -300,7 +347,8 @@ def main(only=None):
         d = run_episode(mod, name, config, es, as_, T, p)
         out = os.path.join(HERE, name + '.npz')
         np.savez_compressed(out, **d)
-        print(f"{name}: steps={len(d['done'])} done={bool(d['done'][-1])} stats={d['stats']} "
+        print(f"{name}: steps={len(d['done'])} done={bool(d['done'][-1])} max_inv={int(d['max_inventory'])} "
+              f"stats={d['stats']} "
               f"-> {os.path.getsize(out) // 1024} KiB", flush=True)
 
 

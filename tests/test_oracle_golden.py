@@ -45,3 +45,15 @@ def test_golden_coverage():
     for k in ['toi_event', 'sleep', 'box_broken', 'box_placed', 'item_picked', 'give_ok', 'give_lost',
               'drop_items', 'heal_used', 'aa_contact']:
         assert c[k] > 0, (k, c)
+
+
+def test_ffal_fixtures_fill_past_four_slots():
+    """The ffal-class fixtures (Inventory with slots > 4, more than 16 heals /
+    4 boxes: semantics.py:165-245) hold inventories longer than the small
+    classes' four slots, recorded from the reference's own Inventory."""
+    names = [f for f in FIXTURES if f.startswith('ffal_')]
+    assert len(names) >= 2
+    for name in names:
+        d, cfg = gr.load(name)
+        assert int(d['max_inventory']) > 4, name
+        assert int(d['max_inventory']) <= cfg['inventory']['slots'], name
