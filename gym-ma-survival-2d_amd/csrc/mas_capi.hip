@@ -311,24 +311,24 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
-    int* phys;  // [N] env list + [1] count (k_phys_fast -> general path) + [1] invalid-action count + [1] k_gen queue + [1] the other count slot + [1] list guard
+    int* phys;  // [N] env list + [1] count (k_pre -> general path) + [1] invalid-action count + [1] last count + [1] list guard
     uint8_t* gen_flag;  // [N] env left the fast path this step
-    int* toi;           // [2] counts + [2][N * 8] SolveTOI (env, agent) lists (8 >= agents of every class)
-    float* sweep;
+    float* sweep;       // A/B builds only (MAS_AB_KERNELS): k_gen_solve -> k_gen_toi
     mas_obs_layout layout;
-    // the split step (launch_step): side stream + fork / join events, made at
+    // the slow split (launch_step): side stream + fork / join events, made at
     // the first mas_step that splits, on the handle's device.  split: 0 the
-    // one-stream order, 1 every general-path env on the side stream
-    // (measured slower), 2 (default) the slow list only; MAS_SPLIT=0/1/2 in
-    // the environment at mas_create, or mas_debug_force_general bits 2 / 3
+    // one-stream order, 2 (default) the slow list on the side stream;
+    // MAS_SPLIT=0/2 in the environment at mas_create, or
+    // mas_debug_force_general bit 3 (one stream)
     StepSplit sp;
     bool sp_made;
     int split, split_default;
+    int* resetl;        // [2][N] auto-reset lists (main, side stream) + [2] counts
     int* slow;          // [N] slow list + [2] count slots
     uint8_t* slow_flag; // [N]
     int* slow_sig;      // host-mapped signal (P.slow_sig): a step flagged a slow env
     int slow_hold;      // steps left of the slow split since the last signal
-    int par;  // which of the two list-count slots the next mas_step appends to
+    int par;  // which of the two slow-list count slots the next mas_step appends to
 };
 
 static void build_layout(mas_handle* h)
@@ -551,7 +551,9 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 8) * sizeof(int));
     if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 8) * sizeof(int));
     h->sweep = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * kToiListAgents * sizeof(float));
+#if MAS_AB_KERNELS
+    if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * kSweepAgents * sizeof(float));
+#endif
     h->P.sweep = h->sweep;
     h->gen_flag = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->gen_flag, (size_t)n_envs);
@@ -560,17 +562,16 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.phys_list = h->phys;
     h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
     h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
-    h->P.gen_next = h->phys ? h->phys + n_envs + 2 : nullptr;
-    h->P.phys_prev = h->phys ? h->phys + n_envs + 3 : nullptr;
+    h->P.phys_last = h->phys ? h->phys + n_envs + 2 : nullptr;
     h->par = 0;
     h->sp_made = false;
     {
         const char* v = getenv("MAS_SPLIT");
-        h->split = h->split_default = (v && v[0] >= '0' && v[0] <= '2') ? v[0] - '0' : 2;
+        h->split = h->split_default = (v && v[0] == '0') ? 0 : 2;
         const char* k = getenv("MAS_SLOW_K");
         h->P.slow_k = k ? atoi(k) : 4;  // TOI events of an env's step that make it slow (the cap always does)
     }
-    h->P.list_overflow = h->phys ? h->phys + n_envs + 4 : nullptr;
+    h->P.list_overflow = h->phys ? h->phys + n_envs + 3 : nullptr;
     h->slow = nullptr;
     h->slow_flag = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->slow, ((size_t)n_envs + 4) * sizeof(int));
@@ -585,6 +586,11 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->slow_hold = 0;
     h->P.slow_sig = nullptr;
     h->P.slow_route = 0;
+    h->resetl = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&h->resetl, ((size_t)2 * n_envs + 2) * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->resetl, 0, ((size_t)2 * n_envs + 2) * sizeof(int));
+    h->P.reset_list = h->resetl;
+    h->P.reset_count = h->resetl ? h->resetl + 2 * n_envs : nullptr;
     h->P.gen_sparse = 0;
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->slow_sig, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) {
@@ -593,11 +599,6 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     }
     h->P.force_general = 0;
     h->P.solve_one_lane = 0;
-    h->toi = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->toi, ((size_t)2 * n_envs * kToiListAgents + 2) * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->toi, 0, ((size_t)2 * n_envs * kToiListAgents + 2) * sizeof(int));
-    h->P.toi_count = h->toi;
-    h->P.toi_list = h->toi ? h->toi + 2 : nullptr;
     h->P.toi_diag = nullptr;
 #ifdef MAS_PROFILE
     if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
@@ -620,9 +621,9 @@ int mas_destroy(mas_handle* h)
     if (h->P.prof) (void)hipFree(h->P.prof);
     if (h->phys) (void)hipFree(h->phys);
     if (h->sweep) (void)hipFree(h->sweep);
-    if (h->toi) (void)hipFree(h->toi);
     if (h->gen_flag) (void)hipFree(h->gen_flag);
     if (h->slow) (void)hipFree(h->slow);
+    if (h->resetl) (void)hipFree(h->resetl);
     if (h->slow_flag) (void)hipFree(h->slow_flag);
     if (h->slow_sig) (void)hipHostFree(h->slow_sig);
     if (h->sp_made) {
@@ -699,28 +700,24 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
         HIP_TRY(e);
         h->sp_made = true;
     }
-    // the two list-count slots alternate: this step appends to one, and its
-    // k_pre zeroes the other (the previous step's) for the next step
+    // The general-path list's count is zeroed on the device after its last
+    // reader (launch_step), so the one-stream step (MAS_SPLIT=0) can be
+    // graph-captured and replayed.  The slow list's two count slots alternate
+    // per step (this step appends to one, its k_pre zeroes the other); the
+    // slow split itself is a host decision per step, so it is never captured.
     Params P = h->P;
-    if (h->par) {
-        std::swap(P.phys_count, P.phys_prev);
-        std::swap(P.slow_count, P.slow_prev);
-    }
+    if (h->par) std::swap(P.slow_count, P.slow_prev);
     // the slow split runs while the general kernels keep flagging slow envs
     // (the signal lags the device by the steps in flight: slow envs persist
     // for many steps); without any, one stream and no fork / join
     const StepSplit* sp = nullptr;
-    if (h->split == 1) {
-        h->sp.slow = 0;
-        sp = &h->sp;
-    } else if (h->split == 2) {
+    if (h->split == 2) {
         if (__atomic_load_n(h->slow_sig, __ATOMIC_RELAXED)) {
             __atomic_store_n(h->slow_sig, 0, __ATOMIC_RELAXED);
             h->slow_hold = 8;
         }
         if (h->slow_hold > 0) {
             --h->slow_hold;
-            h->sp.slow = 1;
             sp = &h->sp;
         }
     } else {
@@ -784,6 +781,8 @@ int mas_set_state(mas_handle* h, const void* src, void* stream)
 {
     if (!h || !src) return fail(MAS_ERR_INVALID_ARG, "mas_set_state: null argument");
     HIP_TRY(hipMemcpyAsync(h->state, src, (size_t)mas_state_bytes(h), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    // the slow-list routing hints belong to the replaced trajectories
+    HIP_TRY(hipMemsetAsync(h->slow_flag, 0, (size_t)h->N, (hipStream_t)stream));
     return MAS_OK;
 }
 
@@ -809,9 +808,9 @@ int mas_debug_counters(mas_handle* h, int64_t* host_out)
     if (!h || !host_out) return fail(MAS_ERR_INVALID_ARG, "mas_debug_counters: null argument");
     int c = 0, c2 = 0;
     HIP_TRY(hipDeviceSynchronize());
-    // the count slots the last mas_step appended to (kept until the next k_pre):
-    // the general-path list and the slow list
-    HIP_TRY(hipMemcpy(&c, h->par ? h->P.phys_count : h->P.phys_prev, sizeof(int), hipMemcpyDeviceToHost));
+    // the last step's general-path count (kept by its first post kernel) and
+    // the slow-list slot it appended to (kept until the next k_pre)
+    HIP_TRY(hipMemcpy(&c, h->P.phys_last, sizeof(int), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&c2, h->par ? h->P.slow_count : h->P.slow_prev, sizeof(int), hipMemcpyDeviceToHost));
     host_out[0] = (int64_t)c + c2;
     return MAS_OK;
@@ -830,9 +829,13 @@ int mas_debug_guards(mas_handle* h, int64_t* host_out)
 int mas_debug_force_general(mas_handle* h, int32_t on)
 {
     if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: null handle");
+#if !MAS_AB_KERNELS
+    if (on & 2) return fail(MAS_ERR_UNSUPPORTED, "mas_debug_force_general: the one-lane kernels are in libmas_ab.so only");
+#endif
+    if (on & 4) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: bit 2 (the all-general split) was removed");
     h->P.force_general = (on & 1) ? 1 : 0;
     h->P.solve_one_lane = (on & 2) ? 1 : 0;
-    h->split = (on & 8) ? 0 : ((on & 4) ? 1 : h->split_default);
+    h->split = (on & 8) ? 0 : h->split_default;
     return MAS_OK;
 }
 

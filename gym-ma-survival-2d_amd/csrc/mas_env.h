@@ -19,6 +19,12 @@
 #include "mas_math.h"
 #include "ziggurat_tables.h"
 
+// 1: test builds (make ab -> libmas_ab.so) with the one-lane general-path
+// kernels of mas_ab.h (scripts/ab_solve_golden.py); 0: the product library
+#ifndef MAS_AB_KERNELS
+#define MAS_AB_KERNELS 0
+#endif
+
 namespace mas {
 
 // damage causes (Health.causes values, semantics.py:490-500)
@@ -31,7 +37,7 @@ constexpr int kNumWalls = 4;
 constexpr int kMaxPhases = 9;   // zone radii incl. the appended 0
 constexpr int kStats = 19;      // MAS_STATS_WIDTH
 constexpr int kMaxLasers = 32;  // MAS_MAX_LASERS
-constexpr int kToiListAgents = 8;  // agents per env the SolveTOI (env, agent) list is sized for (mas_create)
+constexpr int kSweepAgents = 8;  // agents per env of the A/B builds' sweep buffer (mas_create)
 
 template <int AM_, int HM_, int BM_, int SM_, int KC_>
 struct Cap {
@@ -82,26 +88,27 @@ struct Params {
     int n_lasers;
     float lid_depth;
     double lid_off[kMaxLasers];
-    int* phys_list;   // envs that left the contact-free fast path this step (k_phys_fast -> k_phys)
-    int* phys_count;  // number of them: one of two count slots, alternating per mas_step
-    int* phys_prev;   // the other slot (the previous step's count): k_pre zeroes it for the next step
-    int* gen_next;    // k_gen work queue: next chunk of the list (reset by k_post)
-    int* list_overflow;  // appends to phys_list / toi_list refused by their bounds (mas_debug_guards; must stay 0)
+    int* phys_list;   // envs that left the contact-free fast path this step (k_pre -> general path)
+    int* phys_count;  // number of them: appended by k_pre, zeroed by the first post kernel on the caller's
+                      // stream once the general path (its only reader) is done (graph-replay safe)
+    int* phys_last;   // the last step's count, copied there before the zeroing (mas_debug_counters)
+    int* list_overflow;  // appends to phys_list / slow_list / reset_list refused by their bounds (mas_debug_guards)
+    int* reset_list;     // [N] the done envs of this step's post kernel (auto-reset; the side stream: its own list)
+    int* reset_count;    // their count: zeroed by k_pre, appended by k_post_lanes, read by the reset launch
     int force_general;   // test diagnostics (mas_debug_force_general): every env takes the general physics path
-    int solve_one_lane;  // test diagnostics (mas_debug_force_general, on = 2): the one-lane-per-env k_gen_solve
-    int* toi_list;    // [2][N * AM] (env, agent) pairs for k_gen_toi, per world step (k_gen_solve)
-    int* toi_count;   // [2] their counts (reset by k_post)
-    uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (k_phys_fast)
-    float* sweep;     // [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
+    int solve_one_lane;  // A/B builds only (MAS_AB_KERNELS): the one-lane k_gen_solve + k_gen_toi
+    uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (2: on the slow list)
+    float* sweep;     // A/B builds only: [env][3 * agent slots] b2Sweep c0.x, c0.y, a0 (k_gen_solve -> k_gen_toi)
     int* toi_diag;    // test diagnostics (mas_debug_set_toi_counter): per env, TOI events + 65536 per capped SolveTOI
     int* bad_actions; // env-steps whose actions fell outside MultiDiscrete([3,3,3,2,2,2]) (clamped; mas_invalid_actions)
     // the slow split (launch_step): envs whose last general-path step had a
     // SolveTOI that hit the sub-step cap, or >= slow_k TOI events, go to
     // their own list, run on the side stream (k_pre routes, gen_flag 2)
     int* slow_list;      // [N]
-    int* slow_count;     // its count slot this step (alternating, as phys_count)
+    int* slow_count;     // its count slot this step: two slots alternate per split step (the split is
+                         // decided on the host per mas_step, so it is never graph-captured)
     int* slow_prev;      // the other slot: k_pre zeroes it
-    uint8_t* slow_flag;  // [N] set by k_gen_solve_g, read and cleared by k_pre
+    uint8_t* slow_flag;  // [N] set by k_gen_solve_g, read and cleared by k_pre (cleared by resets)
     int slow_k;          // 0: no slow flags
     int slow_route;      // this step routes the flagged envs to the slow list (the slow split is on)
     int* slow_sig;       // host-mapped: set to 1 when k_gen_solve_g flags an env (the host turns the split on)
@@ -111,13 +118,12 @@ struct Params {
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
 
-// The split step (launch_step): a second stream of the handle for the general
-// path and the general envs' post phases, forked from and joined back into
-// the caller's stream by two events.  Null: the one-stream order.
+// The slow split (launch_step): a second stream of the handle for the slow
+// list's general path and post phases, forked from and joined back into the
+// caller's stream by two events.  Null: the one-stream order.
 struct StepSplit {
     hipStream_t side;
     hipEvent_t fork, join;
-    int slow;  // 1: only the slow list on the side stream; 0: every general-path env
 };
 
 // Phase timing for the profiling build (make prof -> libmas_prof.so): lane 0
@@ -231,14 +237,7 @@ constexpr int kLanes = 64;  // one wave per workgroup in every env kernel
 #define MAS_STATE_PAD 0
 #endif
 MAS_HD int64_t state_stride(int64_t N) { return N + MAS_STATE_PAD; }
-#ifndef MAS_STATE_VEC4
-#define MAS_STATE_VEC4 0
-#endif
-#if MAS_STATE_VEC4
-MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (((int64_t)(w >> 2)) * state_stride(N) + e) * 4 + (w & 3); }
-#else
 MAS_HD int64_t state_index(int w, int64_t e, int64_t N) { return (int64_t)w * state_stride(N) + e; }
-#endif
 
 template <class C>
 struct ContLdsStore {  // [word][kLanes] in LDS

@@ -1,7 +1,7 @@
 // mas_gensolve.h -- b2World::Step Collide + island Solve of the general
 // physics path on a lane group per env (k_gen_solve_g, mas_kernels.inc).
 //
-// Same state changes, bit for bit, as world_step_solve (mas_physics.h) --
+// Same state changes, bit for bit, as world_step_solve (mas_ab.h, test builds) --
 // the one-lane-per-env form this replaces, itself the restatement of
 // b2World::Step up to SolveTOI (Box2D 2.3.x b2World::Solve, b2Island::Solve,
 // b2ContactSolver) that oracle/mas_oracle.c pins:
@@ -48,7 +48,6 @@ struct SolveShape {
     static constexpr int KL = C::NAA + C::AM * C::NS;                 // contact records per env
     static constexpr int KR = C::KC < 4 ? C::KC : 4;                  // island contacts held in registers
     static_assert(need <= 32, "one lane per static / agent pair, 32-bit group ballots");
-    static_assert(C::AM <= kToiListAgents, "the sweep buffer holds kToiListAgents agents per env (mas_create)");
 };
 
 // contact record fields in LDS ([field][q][env of the wave])
@@ -146,7 +145,7 @@ __device__ __forceinline__ void group_static(const Params& P, const uint32_t* __
 // iterations (exact fixed-point exit), impulse store, integration, <= 10
 // position iterations with the island's early exit, sleep.  The same
 // operations in the same order as the LDS loops of gen_solve_group (and as
-// world_solve, mas_physics.h).  new_awake: the members still awake.
+// world_solve, mas_ab.h).  new_awake: the members still awake.
 template <class C, class KT>
 __device__ __forceinline__ void island_solve_regs(const Params& P, const SolveRec<C>& R, const KT& K,
                                                   const int (&qi)[SolveShape<C>::KR], int n, uint32_t members, V2 (&c)[C::AM],

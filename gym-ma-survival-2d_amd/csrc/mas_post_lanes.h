@@ -1,0 +1,986 @@
+// mas_post_lanes.h -- the post-physics phases of the MaSurvival step in one
+// launch on agent lanes (gfx950 HIP): the boxes' Health.post_step and
+// despawn, Cameras.post_step, the agents' post_step (deaths + DeathDrop,
+// AutoPickup, SafeZone), rewards, done, stats and the observation rows.
+//
+// Lane (env slot j, agent i) as in k_pre_lanes (mas_lanes.h): C::AM lanes
+// per env, kWG / C::AM envs per wave.  The env's shared groups (boxes,
+// pending drops, box items, heals, the zone) and a table of its agents'
+// poses and healths live in LDS, loaded once per step by cooperative row
+// loads; each lane holds its own agent's rule state.  This replaces three
+// launches (k_cameras, k_post, k_obs) that each reloaded the same groups
+// from HBM: the observation rows are built from the post-step state already
+// in LDS.  Env-level steps whose order is observable (the box compaction,
+// DeathDrop's RNG draws and spawns, the pickup compaction, the zone tick,
+// the stats) run on the env's leader lane (agent 0) over LDS; per-agent
+// steps (the camera cone queries, the pickup lists and takes, the zone
+// damage, the rewards, the contact rows of a dead agent) on the agent's
+// lane.  Same operations on the same values as box_health, update_seen_cam,
+// step_post and write_obs_row (mas_step.h), so the same bits.
+//
+// Reference: masurvival/semantics.py:270-283 (AutoPickup), 387-396
+// (DeathDrop), 403-506 (Health), 704-811 (SafeZone), 853-861 / 907-912
+// (Object / OwnedObject despawn); simulation.py:314-354 (Cameras);
+// envs/masurvival_env.py:510-739 (fetch_observations), 757-831 (rewards,
+// is_done), 483-508 (stats).
+#pragma once
+
+#include "mas_lanes.h"
+
+namespace mas {
+
+constexpr int kPostObsW = 32;  // obs column window of the LDS tile
+
+template <class C>
+struct PostLds {
+    static constexpr int S = kWG / C::AM;  // env slots per wave
+    using LY = Lay<C>;
+    static constexpr int kAgF = 7;                      // agent table: cx cy a vx vy w health
+    static constexpr int kDropW = 3 + 3 * C::SM;        // a dying agent: cx cy n, then (meta hx hy) per slot
+    uint32_t box[LY::kBoxW * S];
+    uint32_t item[LY::kItemW * S];
+    uint32_t heal[LY::kHealW * S];
+    uint32_t zone[LY::kZoneW * S];
+    float ag[kAgF * C::AM * S];  // [field][agent][slot]
+    uint32_t seen[C::NB * S];    // camera-position mask byte per body (low 8 bits)
+    int64_t eidx[S];             // env of each slot
+    uint32_t misc[S];            // per slot: the despawn's kept mask | nbox before << 24 | any dead << 23
+    uint32_t alivem[S];          // per slot: the alive mask the cameras see
+    union {
+        struct {
+            uint16_t list[C::NB * kWG];  // the wave's (camera position, lane, body) ray list
+        } cam;
+        struct {
+            uint32_t drop[kDropW * C::AM * S];  // [field][agent][slot]
+            double ang[C::AM * C::SM * S];       // DeathDrop angles, [k][slot]
+        } dd;
+        float tile[kWG * (kPostObsW + 1)];  // obs rows, one column window
+    } u;
+};
+
+// slot j's view of PostLds
+template <class C>
+struct PostV {
+    static constexpr int S = kWG / C::AM;
+    PostLds<C>* d;
+    int j;
+    __device__ uint32_t& bw(int w) const { return d->box[w * S + j]; }
+    __device__ uint32_t& iw(int w) const { return d->item[w * S + j]; }
+    __device__ uint32_t& hw(int w) const { return d->heal[w * S + j]; }
+    __device__ uint32_t& zw(int w) const { return d->zone[w * S + j]; }
+    __device__ float& ag(int f, int k) const { return d->ag[(f * C::AM + k) * S + j]; }
+    __device__ uint32_t& sn(int body) const { return d->seen[body * S + j]; }
+    __device__ int nbox() const { return (int)bw(0); }
+    __device__ V2 bp(int b) const { return mk(__uint_as_float(bw(1 + 6 * b)), __uint_as_float(bw(2 + 6 * b))); }
+    __device__ float bhx(int b) const { return __uint_as_float(bw(3 + 6 * b)); }
+    __device__ float bhy(int b) const { return __uint_as_float(bw(4 + 6 * b)); }
+    __device__ int bmeta(int b) const { return (int)bw(5 + 6 * b); }
+    __device__ int bhealth(int b) const { return (int)bw(6 + 6 * b); }
+    __device__ int nbi() const { return (int)iw(0); }
+    __device__ V2 ip(int b) const { return mk(__uint_as_float(iw(1 + 5 * b)), __uint_as_float(iw(2 + 5 * b))); }
+    __device__ float ihx(int b) const { return __uint_as_float(iw(3 + 5 * b)); }
+    __device__ float ihy(int b) const { return __uint_as_float(iw(4 + 5 * b)); }
+    __device__ int imeta(int b) const { return (int)iw(5 + 5 * b); }
+    __device__ int nheal() const { return (int)hw(0); }
+    __device__ V2 hp(int h) const { return mk(__uint_as_float(hw(1 + 2 * h)), __uint_as_float(hw(2 + 2 * h))); }
+    __device__ V2 agent(int k) const { return mk(ag(0, k), ag(1, k)); }
+    // zone words (visit_state: zc[9] (x, y), phase, t_cd, t_sh, endgame, zpos, zrad)
+    __device__ V2 zc(int k) const { return mk(__uint_as_float(zw(2 * k)), __uint_as_float(zw(2 * k + 1))); }
+    static constexpr int kZPhase = 2 * kMaxPhases, kZCd = kZPhase + 1, kZSh = kZPhase + 2, kZEnd = kZPhase + 3,
+                         kZPx = kZPhase + 4, kZPy = kZPhase + 5, kZRad = kZPhase + 6;
+};
+
+// env-slot table versions of the cooperative row loads / stores (the slots'
+// envs need not be consecutive: the slow list)
+template <int S>
+__device__ __forceinline__ void slot_load(uint32_t* __restrict__ dst, const uint32_t* __restrict__ state, int64_t N,
+                                          const int64_t* eidx, int w0, int nw)
+{
+    for (int idx = (int)threadIdx.x; idx < nw * S; idx += kWG) {
+        const int w = idx / S, j = idx - w * S;
+        dst[idx] = state[state_index(w0 + w, eidx[j], N)];
+    }
+}
+template <int S>
+__device__ __forceinline__ void slot_store(const uint32_t* __restrict__ src, uint32_t* __restrict__ state, int64_t N,
+                                           const int64_t* eidx, int w0, int nw, uint32_t slots)
+{
+    for (int idx = (int)threadIdx.x; idx < nw * S; idx += kWG) {
+        const int w = idx / S, j = idx - w * S;
+        if ((slots >> j) & 1u) state[state_index(w0 + w, eidx[j], N)] = src[idx];
+    }
+}
+
+// slots whose env-leader lane (agent 0) has b set
+template <class C>
+__device__ __forceinline__ uint32_t slot_mask(bool b)
+{
+    constexpr int S = kWG / C::AM;
+    const uint64_t m = __ballot(b && ((int)threadIdx.x % C::AM) == 0);
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < S; ++q) r |= (uint32_t)((m >> (q * C::AM)) & 1ull) << q;
+    return r;
+}
+
+// ray_cast_fixtab (mas_step.h) with every input read from slot j's LDS
+// groups and agent table instead of a fixture table: the same broadphase
+// cull and the same exact tests in the same canonical order, so the same
+// first hit
+template <class C>
+__device__ __forceinline__ int ray_cast_pv(const Params& P, const PostV<C>& V, uint32_t alive, V2 p1, V2 p2)
+{
+    constexpr float m = 1e-3f;
+    const V2 r = sub(p2, p1);
+    const float rl = len(r);
+    const V2 rn = rl > 0.0f ? scl(1.0f / rl, r) : mk(0.0f, 0.0f);
+    const V2 v = mk(-rn.y, rn.x);
+    const V2 av = mk(fabsf(v.x), fabsf(v.y));
+    const float lox = fminf(p1.x, p2.x) - m, loy = fminf(p1.y, p2.y) - m;
+    const float hix = fmaxf(p1.x, p2.x) + m, hiy = fmaxf(p1.y, p2.y) + m;
+    auto keep = [&](V2 c, float ex, float ey) -> bool {
+        if (c.x - ex > hix || c.x + ex < lox || c.y - ey > hiy || c.y + ey < loy) return false;
+        return fabsf(dot(v, sub(p1, c))) - (av.x * ex + av.y * ey) <= m;
+    };
+    const int nbox = V.nbox(), nbi = V.nbi(), nheal = V.nheal();
+    uint64_t mask = 0;
+    for (int b = 0; b < nbox; ++b)
+        if (keep(V.bp(b), V.bhx(b), V.bhy(b))) mask |= 1ull << (BIdx<C>::box + b);
+    for (int b = 0; b < nbi; ++b)
+        if (keep(V.ip(b), P.bitem_r, P.bitem_r)) mask |= 1ull << (BIdx<C>::bitem + b);
+    for (int h = 0; h < nheal; ++h)
+        if (keep(V.hp(h), P.heal_r, P.heal_r)) mask |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+    for (int w = 0; w < kNumWalls; ++w) {
+        const V2 c = scl(0.5f, add(P.wall_lo[w], P.wall_hi[w]));
+        const V2 e = scl(0.5f, sub(P.wall_hi[w], P.wall_lo[w]));
+        if (keep(c, e.x + m, e.y + m)) mask |= 1ull << (BIdx<C>::wall + w);
+    }
+#pragma unroll
+    for (int k = 0; k < C::AM; ++k)
+        if (bit(alive, k) && keep(V.agent(k), P.agent_r, P.agent_r)) mask |= 1ull << (BIdx<C>::agent + k);
+    float maxf = 1.0f;
+    int hit = -1;
+    while (mask) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        float f;
+        const bool is_box = k < BIdx<C>::bitem;
+        const bool is_wall = k >= BIdx<C>::wall && k < BIdx<C>::agent;
+        if (is_box || is_wall) {
+            Poly4 poly;
+            Rot q = kIdRot;
+            V2 c;
+            if (is_box) {
+                const int meta = V.bmeta(k);
+                poly = box_poly(V.bhx(k), V.bhy(k), box_rot(meta), box_copied(meta));
+                c = V.bp(k);
+            } else {
+                poly = P.wall_poly;
+                const int w = k - BIdx<C>::wall;
+                c = opq(P.wall_pos[0]);
+                q.s = opq(P.wall_q[0].s);
+                q.c = opq(P.wall_q[0].c);
+#pragma unroll
+                for (int q2 = 1; q2 < kNumWalls; ++q2)
+                    if (q2 == w) { c = opq(P.wall_pos[q2]); q.s = opq(P.wall_q[q2].s); q.c = opq(P.wall_q[q2].c); }
+            }
+            f = ray_poly(poly, c, q, p1, p2, maxf);
+        } else {
+            V2 c;
+            float rad;
+            if (k < BIdx<C>::heal) { c = V.ip(k - BIdx<C>::bitem); rad = P.bitem_r; }
+            else if (k < BIdx<C>::wall) { c = V.hp(k - BIdx<C>::heal); rad = P.heal_r; }
+            else { c = V.agent(k - BIdx<C>::agent); rad = P.agent_r; }
+            f = ray_circle(rad, c, p1, p2, maxf);
+        }
+        if (f >= 0.0f) {
+            hit = k;
+            maxf = f;
+            if (maxf == 0.0f) break;
+        }
+    }
+    return hit;
+}
+
+// boxes: Health.post_step + Object / OwnedObject despawn (box_health,
+// mas_step.h) of slot j on LDS, by its leader lane.  Returns whether the
+// box / pending groups changed; kept, nb: the despawn compaction's kept
+// boxes and nbox before it (any_dead: a compaction ran).
+template <class C>
+__device__ __forceinline__ bool box_health_v(const PostV<C>& V, const Params& P, bool& any_dead, uint32_t& kept,
+                                             int& nb, uint32_t* __restrict__ state, int64_t N, int64_t e, bool store)
+{
+    using LY = Lay<C>;
+    bool changed = false;
+    any_dead = false;
+    kept = 0;
+    nb = V.nbox();
+    for (int b = 0; b < nb; ++b) {
+        const int meta = V.bmeta(b);
+        if (!box_hinit(meta)) {
+            V.bw(5 + 6 * b) = (uint32_t)mk_boxmeta(box_rot(meta), box_copied(meta), 1, box_vuln(meta), box_cause(meta));
+            V.bw(6 + 6 * b) = (uint32_t)P.box_health;
+            changed = true;
+        }
+        if (V.bhealth(b) <= 0) any_dead = true;
+        else kept |= 1u << b;
+    }
+    if (any_dead) {
+        changed = true;
+        // stable compaction; dead boxes queue (pos, copy_shape(proto), cause)
+        int wi = 0;
+        for (int b = 0; b < nb; ++b) {
+            const V2 p = V.bp(b);
+            const float hx = V.bhx(b), hy = V.bhy(b);
+            const int meta = V.bmeta(b), hl = V.bhealth(b);
+            if (hl <= 0) {
+                const int rot = box_copy_rot(hx, hy, box_rot(meta));
+                const int pm = mk_bimeta(rot, 1, box_cause(meta));
+                // Object.next_spawns, straight to HBM (the pending group is
+                // otherwise untouched here; k_pre drained it this step)
+                const int np_ = (int)state[state_index(LY::pend, e, N)];
+                if (store) {
+                    if (np_ < C::BM) {
+                        const uint32_t w5[5] = {__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(hx),
+                                                __float_as_uint(hy), (uint32_t)pm};
+#pragma unroll
+                        for (int q = 0; q < 5; ++q) state[state_index(LY::pend + 1 + 5 * np_ + q, e, N)] = w5[q];
+                    }
+                    state[state_index(LY::pend, e, N)] = (uint32_t)(np_ + 1);
+                }
+            } else {
+                if (wi != b) {
+#pragma unroll
+                    for (int q = 1; q <= 6; ++q) V.bw(q + 6 * wi) = V.bw(q + 6 * b);
+                }
+                ++wi;
+            }
+        }
+        V.bw(0) = (uint32_t)wi;
+    }
+    return changed;
+}
+
+// SafeZone.tick (zone_tick, mas_step.h) on slot j's LDS zone words
+template <class C>
+__device__ __forceinline__ void zone_tick_v(const PostV<C>& V, const Params& P)
+{
+    using PV = PostV<C>;
+    int t_cd = (int)V.zw(PV::kZCd), t_sh = (int)V.zw(PV::kZSh), phase = (int)V.zw(PV::kZPhase);
+    const int endgame = (int)V.zw(PV::kZEnd);
+    if (t_cd == 0) {
+        if (endgame) return;
+        t_sh -= 1;
+        V.zw(PV::kZSh) = (uint32_t)t_sh;
+        if (t_sh > 0) {
+            const double t = (double)t_sh / (double)P.zone_cooldown;
+            double r1 = 0.0, r2 = 0.0;
+#pragma unroll
+            for (int k = 0; k + 1 < kMaxPhases; ++k)
+                if (k == phase) { r1 = opq(P.zrad[k]); r2 = opq(P.zrad[k + 1]); }
+            const V2 c1 = V.zc(phase), c2 = V.zc(phase + 1);
+            const double radius = t * r1 + (1.0 - t) * r2;
+            const float tf = (float)t, tf1 = (float)(1.0 - t);
+            const V2 zp = add(scl(tf, c1), scl(tf1, c2));
+            V.zw(PV::kZRad) = __float_as_uint((float)radius);
+            V.zw(PV::kZPx) = __float_as_uint(zp.x);
+            V.zw(PV::kZPy) = __float_as_uint(zp.y);
+            return;
+        }
+        V.zw(PV::kZCd) = (uint32_t)P.zone_cooldown;
+        phase += 1;
+        V.zw(PV::kZPhase) = (uint32_t)phase;
+        const V2 zp = V.zc(phase);
+        V.zw(PV::kZPx) = __float_as_uint(zp.x);
+        V.zw(PV::kZPy) = __float_as_uint(zp.y);
+        float zr = __uint_as_float(V.zw(PV::kZRad));
+#pragma unroll
+        for (int k = 0; k < kMaxPhases; ++k)
+            if (k == phase) zr = opq(P.zradf[k]);
+        V.zw(PV::kZRad) = __float_as_uint(zr);
+        if (phase == P.zone_phases - 1) V.zw(PV::kZEnd) = 1u;
+    } else {
+        t_cd -= 1;
+        V.zw(PV::kZCd) = (uint32_t)t_cd;
+        if (t_cd > 0) return;
+        V.zw(PV::kZSh) = (uint32_t)P.zone_cooldown;
+    }
+}
+
+// The obs row of agent i of slot j (write_obs_row, mas_step.h) from LDS:
+// the agent table (post-step healths), the post-tick zone, the post-pickup
+// heals, boxes and box items and their seen bytes; own: the lane's
+// inventory's last item.  Sink: WinRow-like (column window).
+struct WinRowP {
+    float* p;
+    int c0;
+    __device__ void operator()(int k, float v)
+    {
+        const unsigned kk = (unsigned)(k - c0);
+        p[kk < (unsigned)kPostObsW ? kk : (unsigned)kPostObsW] = v;
+    }
+    __device__ bool want(int off, int len) const { return off < c0 + kPostObsW && off + len > c0; }
+};
+
+template <class C, class Sink>
+__device__ __forceinline__ void write_obs_row_v(const PostV<C>& V, const Params& P, uint32_t alive_m, int i,
+                                                int lastmeta, float lhx, float lhy, Sink& row)
+{
+    using PV = PostV<C>;
+    const int A = P.A, as_ = P.as_;
+    const bool alive = bit(alive_m, i);
+    const int pp = __popc(alive_m & ((1u << i) - 1u));  // post-despawn list position (quirk D1)
+    // agent + others rows (_fetch_agents_observations :659-704)
+    if (row.want(P.o_agent, as_) || row.want(P.o_oth, (A - 1) * as_) || row.want(P.o_othm, A - 1)) {
+        for (int k = 0; k < A; ++k) {
+            const bool ak = bit(alive_m, k);
+            const int ok = k < i ? k : k - 1;
+            int o = k == i ? P.o_agent : P.o_oth + ok * as_;
+            if (!row.want(o, as_) && !(k != i && row.want(P.o_othm + ok, 1))) continue;
+            row(o++, (float)k);
+            if (P.teams) row(o++, (float)team_of(P, k));
+            row(o++, ak ? V.ag(6, k) : 0.0f);
+#pragma unroll
+            for (int f = 0; f < 6; ++f) row(o++, ak ? V.ag(f, k) : 0.0f);
+            if (k != i) {
+                // others_mask: seen list at the post-despawn list index (quirk D1)
+                float m = 1.0f;
+                if (alive && ak && (V.sn(BIdx<C>::agent + k) >> pp) & 1u) m = 0.0f;
+                row(P.o_othm + ok, m);
+            }
+        }
+    }
+    if (row.want(P.o_zone, 6)) {
+        const int phase = (int)V.zw(PV::kZPhase);
+        row(P.o_zone + 0, __uint_as_float(V.zw(PV::kZPx)));
+        row(P.o_zone + 1, __uint_as_float(V.zw(PV::kZPy)));
+        row(P.o_zone + 2, __uint_as_float(V.zw(PV::kZRad)));
+        float z3 = 0.0f, z4 = 0.0f, z5 = 0.0f;
+        if (phase < P.zone_phases - 1) {
+            const V2 zn = V.zc(phase + 1);
+            z3 = zn.x;
+            z4 = zn.y;
+#pragma unroll
+            for (int k = 0; k < kMaxPhases; ++k)
+                if (k == phase + 1) z5 = opq(P.zradf[k]);
+        }
+        row(P.o_zone + 3, z3);
+        row(P.o_zone + 4, z4);
+        row(P.o_zone + 5, z5);
+    }
+    if (P.H > 0 && (row.want(P.o_heal, 2 * P.H) || row.want(P.o_healm, P.H))) {
+        const int nh = V.nheal();
+        for (int h = 0; h < P.H; ++h) {
+            if (!row.want(P.o_heal + 2 * h, 2) && !row.want(P.o_healm + h, 1)) continue;
+            const bool present = h < nh;
+            const V2 hp = V.hp(h);
+            row(P.o_heal + 2 * h, present ? hp.x : 0.0f);
+            row(P.o_heal + 2 * h + 1, present ? hp.y : 0.0f);
+            float m;
+            if (P.omniscient) m = present ? 0.0f : 1.0f;
+            else m = (present && alive && ((V.sn(BIdx<C>::heal + h) >> pp) & 1u)) ? 0.0f : 1.0f;
+            row(P.o_healm + h, m);
+        }
+    }
+    if (P.B > 0 && (row.want(P.o_box, 11 * P.B) || row.want(P.o_boxm, P.B))) {
+        const int nb = V.nbox();
+        for (int b = 0; b < P.B; ++b) {
+            const bool present = b < nb;
+            if (row.want(P.o_box + 11 * b, 11)) {
+                const int meta = V.bmeta(b);
+                const Poly4 poly = box_poly(V.bhx(b), V.bhy(b), box_rot(meta), box_copied(meta));
+                const V2 bp = V.bp(b);
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    row(P.o_box + 11 * b + 2 * v, present ? poly.v[v].x : 0.0f);
+                    row(P.o_box + 11 * b + 2 * v + 1, present ? poly.v[v].y : 0.0f);
+                }
+                row(P.o_box + 11 * b + 8, present ? bp.x : 0.0f);
+                row(P.o_box + 11 * b + 9, present ? bp.y : 0.0f);
+                row(P.o_box + 11 * b + 10, 0.0f);  // box bodies always have angle 0
+            }
+            if (!row.want(P.o_boxm + b, 1)) continue;
+            float m;
+            if (P.omniscient) m = present ? 0.0f : 1.0f;
+            else m = (present && alive && ((V.sn(BIdx<C>::box + b) >> pp) & 1u)) ? 0.0f : 1.0f;
+            row(P.o_boxm + b, m);
+        }
+    }
+    if (P.B > 0 && (row.want(P.o_bi, 10 * P.B) || row.want(P.o_bim, P.B))) {
+        const int ni = V.nbi();
+        for (int b = 0; b < P.B; ++b) {
+            const bool present = b < ni;
+            if (row.want(P.o_bi + 10 * b, 10)) {
+                const float hx = V.ihx(b), hy = V.ihy(b);
+                const int rot = bi_rot(V.imeta(b));
+                const V2 ip = V.ip(b);
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const V2 cv = box_corner(hx, hy, rot + v);
+                    row(P.o_bi + 10 * b + 2 * v, present ? cv.x : 0.0f);
+                    row(P.o_bi + 10 * b + 2 * v + 1, present ? cv.y : 0.0f);
+                }
+                row(P.o_bi + 10 * b + 8, present ? ip.x : 0.0f);
+                row(P.o_bi + 10 * b + 9, present ? ip.y : 0.0f);
+            }
+            if (!row.want(P.o_bim + b, 1)) continue;
+            float m;
+            if (P.omniscient) m = present ? 0.0f : 1.0f;
+            else m = (present && alive && ((V.sn(BIdx<C>::bitem + b) >> pp) & 1u)) ? 0.0f : 1.0f;
+            row(P.o_bim + b, m);
+        }
+    }
+    // lidars: zeros here; k_lidar writes the columns afterwards
+    if (P.n_lasers > 0 && row.want(P.o_lid, P.n_lasers)) {
+        for (int k = 0; k < P.n_lasers; ++k) row(P.o_lid + k, 0.0f);
+    }
+    // usable inventory slots (:620-654)
+    if (row.want(P.o_hs, 1) || row.want(P.o_hsm, 1) || row.want(P.o_bs, 8) || row.want(P.o_bsm, 1)) {
+        if (P.H > 0) {
+            const bool isheal = it_kind(lastmeta) == kItemHeal;
+            row(P.o_hs, isheal ? (float)P.healing : 0.0f);
+            row(P.o_hsm, isheal ? 0.0f : 1.0f);
+        }
+        if (P.B > 0) {
+            const bool isbox = it_kind(lastmeta) == kItemBox;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const V2 cv = box_corner(lhx, lhy, it_rot(lastmeta) + v);
+                row(P.o_bs + 2 * v, isbox ? cv.x : 0.0f);
+                row(P.o_bs + 2 * v + 1, isbox ? cv.y : 0.0f);
+            }
+            row(P.o_bsm, isbox ? 0.0f : 1.0f);
+        }
+    }
+}
+
+
+// The post-physics phases of one step on agent lanes (see the file comment),
+// over env selection M (kAllEnvs / kMainEnvs on the caller's stream, the
+// slow list's kGenEnvs on the side stream).  Done envs are appended to the
+// selection's reset list (auto-reset: the k_obs reset launch over that list
+// follows, launch_post).
+template <class C, int M>
+__global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __restrict__ state, int64_t N,
+                                                       float* __restrict__ obs, float* __restrict__ rew,
+                                                       uint8_t* __restrict__ done, int ar)
+{
+    using LY = Lay<C>;
+    using PV = PostV<C>;
+    constexpr int S = kWG / C::AM, AM = C::AM;
+    static_assert(kWG % AM == 0 && (AM & (AM - 1)) == 0, "agent lane groups must tile a wave");
+    static_assert(C::NB <= 64 && AM <= 8, "16-bit camera list entries, 64-bit body masks");
+    __shared__ PostLds<C> lds;
+    retire_phys_count<M>(P);
+    const int lane = (int)threadIdx.x;
+    const int j = lane / AM, i = lane - j * AM;
+    const int A = P.A;
+    // the env of slot j (lanes past the last env, or of an env the other
+    // stream owns, stay for the wave's collectives and store nothing)
+    const int64_t cnt = gen_list_count<M>(P, N);
+    const int64_t k0 = (int64_t)blockIdx.x * S;
+    if (M == kGenEnvs && k0 >= cnt) return;  // the whole workgroup (one wave)
+    bool valid = k0 + j < cnt;
+    const int64_t e = M == kGenEnvs ? (int64_t)P.phys_list[valid ? k0 + j : k0] : (valid ? k0 + j : N - 1);
+    if (valid && other_stream<M>(P, e)) valid = false;
+    if (i == 0) lds.eidx[j] = e;
+    wave_lds_sync();
+    const PV V{&lds, j};
+    // ---- state: the env-shared groups into LDS, this lane's agent into registers
+    slot_load<S>(lds.box, state, N, lds.eidx, LY::box, LY::kBoxW);
+    slot_load<S>(lds.item, state, N, lds.eidx, LY::item, LY::kItemW);
+    slot_load<S>(lds.heal, state, N, lds.eidx, LY::heal, LY::kHealW);
+    slot_load<S>(lds.zone, state, N, lds.eidx, LY::zone, LY::kZoneW);
+    AgentL<C> g;
+    {
+        float d[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) d[q] = __uint_as_float(state[state_index(7 * i + q, e, N)]);
+        g.c = mk(d[0], d[1]);
+        g.a = d[2];
+        g.v = mk(d[3], d[4]);
+        g.w = d[5];
+        g.sleep = 0.0f;  // (not read here)
+        const int wr = LY::rule + i * LY::kRuleA;
+        g.health = (int)state[state_index(wr, e, N)];
+        g.cause = (int)state[state_index(wr + 1, e, N)];
+        g.cooldown = (int)state[state_index(wr + 2, e, N)];
+        g.inv_n = (int)state[state_index(wr + 3, e, N)];
+#pragma unroll
+        for (int k = 0; k < C::SM; ++k) {
+            g.inv_meta[k] = (int)state[state_index(wr + 4 + 3 * k, e, N)];
+            g.inv_hx[k] = __uint_as_float(state[state_index(wr + 5 + 3 * k, e, N)]);
+            g.inv_hy[k] = __uint_as_float(state[state_index(wr + 6 + 3 * k, e, N)]);
+        }
+    }
+    uint32_t alive_m = state[state_index(LY::alive, e, N)];
+    uint32_t awake_m = state[state_index(LY::awake, e, N)];
+    bool alive = bit(alive_m, i);
+    V.ag(0, i) = g.c.x;
+    V.ag(1, i) = g.c.y;
+    V.ag(2, i) = g.a;
+    V.ag(3, i) = g.v.x;
+    V.ag(4, i) = g.v.y;
+    V.ag(5, i) = g.w;
+    wave_lds_sync();  // the wave's LDS groups are loaded (one-wave block)
+    MAS_PROF(P, 34);
+    // ---- boxes: Health.post_step + despawn (the first post_step hook, dict
+    // order: the boxes group before the agents)
+    bool bchanged = false;
+    if (i == 0) {
+        bool any_dead;
+        uint32_t kept;
+        int nb;
+        bchanged = box_health_v(V, P, any_dead, kept, nb, state, N, e, valid);
+        lds.misc[j] = kept | ((uint32_t)nb << 24) | (any_dead ? (1u << 23) : 0u);
+    }
+    wave_lds_sync();
+    {
+        // the agent-static contact rows follow the boxes (each agent's row on
+        // its own lane: the rows are independent)
+        const uint32_t mj = lds.misc[j];
+        if (valid && (mj & (1u << 23))) {
+            const Cont<C, ContGlbStore<C>> KG{{state, N, e, P.w_cont}};
+            compact_cont_row<C>(KG, i, mj & 0x7fffffu, (int)(mj >> 24));
+        }
+    }
+    // ---- Cameras.post_step (simulation.py:314-354): camera i of slot j
+    {
+        if (i == 0) {
+            lds.alivem[j] = alive_m;
+#pragma unroll
+            for (int k = 0; k < C::NB; ++k) V.sn(k) = 0u;
+        }
+        uint64_t cand = 0;  // bit per body in the cone
+        int p = 0;
+        if (valid && alive) {
+            p = __popc(alive_m & ((1u << i) - 1u));
+            const V2 pos = g.c;
+            const Rot q = rot_of(g.a);
+            const int nb = V.nbox(), ni = V.nbi(), nh = V.nheal();
+            for (int b = 0; b < nb; ++b)
+                if (poly_test_point(P.cone, pos, q, V.bp(b))) cand |= 1ull << (BIdx<C>::box + b);
+            for (int b = 0; b < ni; ++b)
+                if (poly_test_point(P.cone, pos, q, V.ip(b))) cand |= 1ull << (BIdx<C>::bitem + b);
+            for (int h = 0; h < nh; ++h)
+                if (poly_test_point(P.cone, pos, q, V.hp(h))) cand |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+            for (int w = 0; w < kNumWalls; ++w)
+                if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) cand |= 1ull << (BIdx<C>::wall + w);
+#pragma unroll
+            for (int k = 0; k < AM; ++k)
+                if (k != i && bit(alive_m, k) && poly_test_point(P.cone, pos, q, V.agent(k)))
+                    cand |= 1ull << (BIdx<C>::agent + k);
+        }
+        // the wave's rays dealt over its lanes (update_seen_cam)
+        const int np = __popcll(cand);
+        int incl = np;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const int total = __shfl(incl, 63, 64);
+        int at = incl - np;
+        while (cand) {
+            const int body = __builtin_ctzll(cand);
+            cand &= cand - 1;
+            lds.u.cam.list[at++] = (uint16_t)((p << 12) | (lane << 6) | body);
+        }
+        wave_lds_sync();  // the list, the fixture tables and the zeroed seen rows are visible
+        const float eps1 = (float)(1.0 + 1e-6);
+        for (int t = lane; t < total; t += 64) {
+            const uint32_t en = lds.u.cam.list[t];
+            const int body = (int)(en & 63u), o = (int)((en >> 6) & 63u), pc = (int)(en >> 12);
+            const int so = o / AM, co = o - so * AM;  // the owner's slot and camera
+            const PV Vo{&lds, so};
+            const V2 opos = Vo.agent(co);
+            V2 oc;
+            if (body < BIdx<C>::bitem) oc = Vo.bp(body);
+            else if (body < BIdx<C>::heal) oc = Vo.ip(body - BIdx<C>::bitem);
+            else if (body < BIdx<C>::wall) oc = Vo.hp(body - BIdx<C>::heal);
+            else if (body < BIdx<C>::agent) {
+                const int w = body - BIdx<C>::wall;
+                oc = opq(P.wall_pos[0]);
+#pragma unroll
+                for (int q2 = 1; q2 < kNumWalls; ++q2)
+                    if (q2 == w) oc = opq(P.wall_pos[q2]);
+            } else oc = Vo.agent(body - BIdx<C>::agent);
+            const V2 d = sub(oc, opos);
+            const V2 end = add(opos, scl(eps1, d));
+            if (ray_cast_pv(P, Vo, lds.alivem[so], opos, end) == body) atomicOr(&lds.seen[body * S + so], 1u << pc);
+        }
+        wave_lds_sync();  // the seen rows are complete
+    }
+    MAS_PROF(P, 35);
+    // ---------------- agents post_step (step_post, mas_step.h) ----------------
+    uint32_t dirty = kGZone | kGStat;
+    // Health.post_step -> despawn dead (id order): TrackDeaths, IndexBodies,
+    // DeathDrop (semantics.py:387-396), Inventory, Health.pre_despawn -> TrackKills
+    const bool dies = valid && alive && g.health <= 0;
+    const uint32_t died = env_ballot<C>(dies);
+    int kill_cause = kCauseNone;
+    if (__any(died != 0u)) {
+        // the dying agents' positions and inventories for the leader's DeathDrop
+        constexpr int DW = PostLds<C>::kDropW;
+        uint32_t* dr = lds.u.dd.drop;
+        auto dref = [&](int f, int k) -> uint32_t& { return dr[(f * AM + k) * S + j]; };
+        if (dies) {
+            dref(0, i) = __float_as_uint(g.c.x);
+            dref(1, i) = __float_as_uint(g.c.y);
+            dref(2, i) = (uint32_t)g.inv_n;
+#pragma unroll
+            for (int k = 0; k < C::SM; ++k) {
+                dref(3 + 3 * k, i) = (uint32_t)g.inv_meta[k];
+                dref(4 + 3 * k, i) = __float_as_uint(g.inv_hx[k]);
+                dref(5 + 3 * k, i) = __float_as_uint(g.inv_hy[k]);
+            }
+        }
+        (void)DW;
+        wave_lds_sync();
+        if (i == 0 && died) {
+            // numpy Generator(PCG64) of the env: angles = 2*pi*rng.random(total),
+            // popped from the end per dying body (bodies in id order, items in
+            // slot order)
+            EnvL<C> R;
+            {
+                Loader ld{state, N, e, 0};
+                visit_state(R, ld, kGRng);
+            }
+            int total = 0;
+            for (int k = 0; k < AM; ++k)
+                if (bit(died, k)) total += (int)dref(2, k);
+            double* ang = lds.u.dd.ang;
+            for (int k = 0; k < total; ++k) ang[k * S + j] = 6.283185307179586 * pcg_random(R);
+            int top = total;
+            for (int k = 0; k < AM; ++k) {
+                if (!bit(died, k)) continue;
+                const V2 ck = mk(__uint_as_float(dref(0, k)), __uint_as_float(dref(1, k)));
+                const int n = (int)dref(2, k);
+                for (int q = 0; q < n; ++q) {
+                    --top;
+                    const float a = (float)ang[top * S + j];
+                    const V2 off = from_polar(P.dd_r, a);
+                    const V2 pos = add(ck, off);
+                    const int meta = (int)dref(3 + 3 * q, k);
+                    if (it_kind(meta) == kItemHeal) {
+                        const int nh = V.nheal();
+                        if (nh < C::HM) {
+                            V.hw(1 + 2 * nh) = __float_as_uint(pos.x);
+                            V.hw(2 + 2 * nh) = __float_as_uint(pos.y);
+                            V.hw(0) = (uint32_t)(nh + 1);
+                        }
+                    } else {
+                        const int ni = V.nbi();
+                        if (ni < C::BM) {
+                            V.iw(1 + 5 * ni) = __float_as_uint(pos.x);
+                            V.iw(2 + 5 * ni) = __float_as_uint(pos.y);
+                            V.iw(3 + 5 * ni) = dref(4 + 3 * q, k);
+                            V.iw(4 + 5 * ni) = dref(5 + 3 * q, k);
+                            V.iw(5 + 5 * ni) = (uint32_t)mk_bimeta(it_rot(meta), it_copied(meta), it_owner(meta));
+                            V.iw(0) = (uint32_t)(ni + 1);
+                        }
+                    }
+                }
+            }
+            if (valid) {
+                Storer st{state, N, e, 0};
+                visit_state(R, st, kGRng);
+            }
+            // the agent-agent touching word: the pairs of the dead agents
+            const Cont<C, ContGlbStore<C>> KG{{state, N, e, P.w_cont}};
+            uint32_t aat = KG.aat();
+            for (int k = 0; k < AM; ++k) {
+                if (!bit(died, k)) continue;
+                for (int m = 0; m < AM; ++m) {
+                    if (m == k) continue;
+                    const int pi = m < k ? aa_index<C::AM>(m, k) : aa_index<C::AM>(k, m);
+                    aat &= ~(1u << pi);
+                    if (valid) {
+                        KG.set_aani(pi, 0.0f);
+                        KG.set_aati(pi, 0.0f);
+                    }
+                }
+            }
+            if (valid) KG.set_aat(aat);
+        }
+        wave_lds_sync();
+        if (dies) {
+            kill_cause = g.cause;
+            // the dead agent's contact rows (its own lane)
+            const Cont<C, ContGlbStore<C>> KG{{state, N, e, P.w_cont}};
+            KG.set_ast(i, 0u);
+#pragma unroll
+            for (int s = 0; s < C::NS; ++s) {
+                KG.set_asni(i, s, 0.0f);
+                KG.set_asti(i, s, 0.0f);
+            }
+            g.inv_n = 0;
+        }
+        alive_m &= ~died;
+        awake_m &= ~died;
+        alive = bit(alive_m, i);
+        if (died) dirty |= kGDyn | kGRule | kGItem | kGHeal | kGSeen | kGRng;
+    }
+    // AutoPickup.post_step (semantics.py:278-283): every agent's list first,
+    // then the takes in agent order (each agent's own inventory)
+    {
+        uint32_t lb = 0, lh = 0;
+        if (alive) {
+            const int ni = V.nbi(), nh = V.nheal();
+            for (int b = 0; b < ni; ++b)
+                if (circle_test_point(P.pickup_r, g.c, V.ip(b))) lb |= 1u << b;
+            for (int h = 0; h < nh; ++h)
+                if (circle_test_point(P.pickup_r, g.c, V.hp(h))) lh |= 1u << h;
+        }
+        uint32_t takenb = 0, takenh = 0;
+        while (lb) {
+            const int b = __builtin_ctz(lb);
+            lb &= lb - 1;
+            const int im = V.imeta(b);
+            if (1 + g.inv_n <= P.slots) {
+                own_take(g, P, mk_itmeta(kItemBox, bi_rot(im), bi_copied(im), bi_owner(im)), V.ihx(b), V.ihy(b));
+                takenb |= 1u << b;
+            }
+        }
+        while (lh) {
+            const int h = __builtin_ctz(lh);
+            lh &= lh - 1;
+            if (1 + g.inv_n <= P.slots) {
+                own_take(g, P, mk_itmeta(kItemHeal, 0, 0, kCauseNone), 0.0f, 0.0f);
+                takenh |= 1u << h;
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < AM; o <<= 1) {
+            takenb |= (uint32_t)__shfl_xor((int)takenb, o, 64);
+            takenh |= (uint32_t)__shfl_xor((int)takenh, o, 64);
+        }
+        if (takenb | takenh) dirty |= kGRule | kGItem | kGHeal | kGSeen;
+        wave_lds_sync();  // every lane's pickup reads are done
+        if (i == 0 && takenb) {
+            const int ni = V.nbi();
+            int wi = 0;
+            for (int b = 0; b < ni; ++b) {
+                if (bit(takenb, b)) continue;
+                if (wi != b) {
+#pragma unroll
+                    for (int q = 1; q <= 5; ++q) V.iw(q + 5 * wi) = V.iw(q + 5 * b);
+                }
+                V.sn(BIdx<C>::bitem + wi) = V.sn(BIdx<C>::bitem + b);
+                ++wi;
+            }
+            V.iw(0) = (uint32_t)wi;
+        }
+        if (i == 0 && takenh) {
+            const int nh = V.nheal();
+            int wi = 0;
+            for (int h = 0; h < nh; ++h) {
+                if (bit(takenh, h)) continue;
+                if (wi != h) {
+                    V.hw(1 + 2 * wi) = V.hw(1 + 2 * h);
+                    V.hw(2 + 2 * wi) = V.hw(2 + 2 * h);
+                }
+                V.sn(BIdx<C>::heal + wi) = V.sn(BIdx<C>::heal + h);
+                ++wi;
+            }
+            V.hw(0) = (uint32_t)wi;
+        }
+    }
+    // SafeZone.post_step (semantics.py:758-768): damage outliers, then tick
+    if (alive) {
+        const V2 zp = mk(__uint_as_float(V.zw(PV::kZPx)), __uint_as_float(V.zw(PV::kZPy)));
+        const float zr = __uint_as_float(V.zw(PV::kZRad));
+        if (V.zw(PV::kZEnd) || !circle_test_point(zr, zp, g.c)) {
+            own_damage(g, alive, P, i, -P.zone_damage, kCauseZone);
+            dirty |= kGRule;
+        }
+    }
+    wave_lds_sync();  // every lane has read the pre-tick zone
+    if (i == 0) zone_tick_v(V, P);
+    // ---------------- compute_rewards (masurvival_env.py:757-803) ----------------
+    float r = 0.0f;
+    int my_kills = 0, tkills0 = 0, tkills1 = 0;
+    if (!P.teams) {
+        int first_dead = -1;
+        for (int k = AM - 1; k >= 0; --k)
+            if (k < A && !bit(alive_m, k)) first_dead = k;
+        r += bit(alive_m, i) ? P.r_alive : P.r_dead;
+#pragma unroll
+        for (int k = 0; k < AM; ++k) {
+            const int c = env_bcast<C>(kill_cause, k);
+            if (!bit(died, k)) continue;
+            int idx = -1;
+            if (c >= 0 && c < AM && bit(alive_m, c)) idx = c;
+            else if (c == kCauseNone && first_dead >= 0) idx = first_dead;  // None in indexed_agents
+            if (idx == i) {
+                r += P.r_kill;
+                my_kills += 1;
+            }
+        }
+        if (bit(died, i)) r += P.r_death;
+    } else {
+        bool talive0 = false, talive1 = false;
+        for (int k = 0; k < A; ++k)
+            if (bit(alive_m, k)) (team_of(P, k) == 0 ? talive0 : talive1) = true;
+        const int ti = team_of(P, i);
+        if (i < A) r += (ti == 0 ? talive0 : talive1) ? P.r_alive : P.r_dead;
+#pragma unroll
+        for (int k = 0; k < AM; ++k) {
+            const int c = env_bcast<C>(kill_cause, k);
+            if (!bit(died, k)) continue;
+            if (c != kCauseBadge && c != kCauseBadge + 1) continue;
+            const int t = c - kCauseBadge;
+            if (i < A && ti == t) r += P.r_kill;
+            if (t == 0) tkills0 += 1;
+            else tkills1 += 1;
+        }
+#pragma unroll
+        for (int k = 0; k < AM; ++k) {
+            if (!bit(died, k)) continue;
+            if (i < A && ti == team_of(P, k)) r += P.r_death;
+        }
+    }
+    if (valid && i < A) rew[e * A + i] = r;
+    // ---------------- is_done (masurvival_env.py:810-831) ----------------
+    int n_alive = 0;
+    if (P.teams) {
+        bool t0 = false, t1 = false;
+        for (int k = 0; k < A; ++k) {
+            if (!bit(alive_m, k)) continue;
+            if (team_of(P, k) == 0) t0 = true;
+            else t1 = true;
+        }
+        n_alive = (t0 ? 1 : 0) + (t1 ? 1 : 0);
+    } else {
+        n_alive = __popc(alive_m);
+    }
+    const bool is_done = P.gameover == 1 ? (n_alive <= 1) : (n_alive == 0);
+    // ---------------- _update_stats (masurvival_env.py:483-508) ----------------
+    {
+        const int R = P.teams ? 2 : A;
+        float rq[8];
+        int kq[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int jq = P.teams ? (q == 0 ? 0 : A / 2) : q;
+            rq[q] = env_bcast<C>(r, jq < AM ? jq : 0);
+            kq[q] = P.teams ? (q == 0 ? tkills0 : tkills1) : env_bcast<C>(my_kills, q < AM ? q : 0);
+        }
+        if (valid && i == 0) {
+            done[e] = is_done ? 1 : 0;
+            float* st = reinterpret_cast<float*>(state);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (q >= R) continue;
+                st[state_index(LY::stat + q, e, N)] += rq[q];
+                st[state_index(LY::stat + 8 + q, e, N)] += (float)kq[q];
+            }
+            st[state_index(LY::stat + 16, e, N)] += 1.0f;
+        }
+    }
+    MAS_PROF(P, 36);
+    // ---------------- stores: the groups this step changed ----------------
+    uint32_t dirty_env = dirty;
+#pragma unroll
+    for (int o = 1; o < AM; o <<= 1) dirty_env |= (uint32_t)__shfl_xor((int)dirty_env, o, 64);
+    if (valid) {
+        if (dirty_env & kGRule) {
+            const int wr = LY::rule + i * LY::kRuleA;
+            state[state_index(wr, e, N)] = (uint32_t)g.health;
+            state[state_index(wr + 1, e, N)] = (uint32_t)g.cause;
+            state[state_index(wr + 2, e, N)] = (uint32_t)g.cooldown;
+            state[state_index(wr + 3, e, N)] = (uint32_t)g.inv_n;
+#pragma unroll
+            for (int k = 0; k < C::SM; ++k) {
+                state[state_index(wr + 4 + 3 * k, e, N)] = (uint32_t)g.inv_meta[k];
+                state[state_index(wr + 5 + 3 * k, e, N)] = __float_as_uint(g.inv_hx[k]);
+                state[state_index(wr + 6 + 3 * k, e, N)] = __float_as_uint(g.inv_hy[k]);
+            }
+        }
+        if ((dirty_env & kGDyn) && i == 0) {
+            state[state_index(LY::alive, e, N)] = alive_m;
+            state[state_index(LY::awake, e, N)] = awake_m;
+        }
+        if (i == 0) {
+            // the seen bytes (recomputed every step by the cameras)
+#pragma unroll
+            for (int w = 0; w < kSeenWords<C>; ++w) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (4 * w + q < C::NB) x |= (V.sn(4 * w + q) & 0xffu) << (8 * q);
+                state[state_index(LY::seen + w, e, N)] = x;
+            }
+        }
+    }
+    {
+        const uint32_t sv = slot_mask<C>(valid);
+        const uint32_t sb = slot_mask<C>(valid && bchanged);
+        const uint32_t si = slot_mask<C>(valid && (dirty_env & kGItem));
+        const uint32_t sh = slot_mask<C>(valid && (dirty_env & kGHeal));
+        if (sb) slot_store<S>(lds.box, state, N, lds.eidx, LY::box, LY::kBoxW, sb);
+        if (si) slot_store<S>(lds.item, state, N, lds.eidx, LY::item, LY::kItemW, si);
+        if (sh) slot_store<S>(lds.heal, state, N, lds.eidx, LY::heal, LY::kHealW, sh);
+        if (sv) slot_store<S>(lds.zone, state, N, lds.eidx, LY::zone, LY::kZoneW, sv);
+    }
+    // ---------------- auto-reset list: the done envs ----------------
+    if (ar) {
+        const bool mine = valid && i == 0 && is_done;
+        const uint64_t m = __ballot(mine);
+        if (m) {
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(P.reset_count, __popcll(m));
+            base = __shfl(base, leader, 64);
+            if (mine) {
+                const int64_t at = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+                if (at < N) P.reset_list[at] = (int)e;
+                else atomicAdd(P.list_overflow, 1);
+            }
+        }
+    }
+    MAS_PROF(P, 37);
+    // ---------------- fetch_observations: rows from LDS ----------------
+    V.ag(6, i) = (float)g.health;
+    int lastmeta = 0;
+    float lhx = 0.0f, lhy = 0.0f;
+    if (alive && g.inv_n > 0) {
+        lastmeta = sel(g.inv_meta, g.inv_n - 1);
+        lhx = sel(g.inv_hx, g.inv_n - 1);
+        lhy = sel(g.inv_hy, g.inv_n - 1);
+    }
+    wave_lds_sync();  // the agent table's healths and every LDS group are final
+    const int D = P.D;
+    const bool row_on = valid && i < A;
+    const int trow = j * A + i;  // tile row (the wave's rows are consecutive unless kGenEnvs)
+    const int64_t r0 = M == kGenEnvs ? 0 : k0 * A;
+    const int64_t rr = e * A + i;  // this lane's obs row
+    const uint64_t act = __ballot(row_on);
+    float* row_tile = lds.u.tile + trow * (kPostObsW + 1);
+    for (int c0 = 0; c0 < D; c0 += kPostObsW) {
+        if (row_on) {
+            WinRowP sink{row_tile, c0};
+            write_obs_row_v(V, P, alive_m, i, lastmeta, lhx, lhy, sink);
+        }
+        wave_lds_sync();  // the tile's rows are in LDS
+        // lane = (row half, column): rows q and q + 1 per instruction pair
+        const int col = lane & (kPostObsW - 1), half = lane / kPostObsW;
+        const bool col_ok = c0 + col < D;
+        for (int q = half; q < kWG; q += 2) {
+            if (q >= S * A) break;
+            // tile row q: slot q / A, agent q % A
+            const int sq = q / A, aq = q - sq * A;
+            const bool on = (act >> (sq * AM + aq)) & 1ull;
+            if (!on || !col_ok) continue;
+            const int64_t orow = M == kGenEnvs ? lds.eidx[sq] * A + aq : r0 + q;
+            obs[orow * D + c0 + col] = lds.u.tile[q * (kPostObsW + 1) + col];
+        }
+        wave_lds_sync();  // the tile's reads are done before the next window's rows
+    }
+    (void)rr;
+    MAS_PROF(P, 38);
+}
+
+}  // namespace mas

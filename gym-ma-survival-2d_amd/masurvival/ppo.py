@@ -448,7 +448,23 @@ class FusedAdam:
     their gradients and both Adam moments become views into four flat fp32
     buffers; the torch.optim.Adam object keeps holding them as its state, so
     its state_dict (checkpoints) is unchanged.  bind_state() re-points that
-    state after Adam.load_state_dict replaced it."""
+    state after Adam.load_state_dict replaced it.
+
+    Used only for the plain form it restates (supports()): one param group,
+    a float lr, no weight decay, amsgrad, maximize or capturable state; any
+    other optimizer setup stays on torch.  After step(), ``.grad`` of each
+    parameter holds the raw summed minibatch gradient the kernel read (the
+    1 / world scale and the clip are applied inside the kernel, not written
+    back), unlike torch's clip_grad_norm_, which scales .grad in place."""
+
+    @staticmethod
+    def supports(opt) -> bool:
+        if not isinstance(opt, torch.optim.Adam) or len(opt.param_groups) != 1:
+            return False
+        g = opt.param_groups[0]
+        return (not g.get('weight_decay', 0) and not g.get('amsgrad', False) and not g.get('maximize', False)
+                and not g.get('capturable', False) and not g.get('differentiable', False)
+                and not isinstance(g['lr'], torch.Tensor))
 
     def __init__(self, params, opt: torch.optim.Adam, lib, device):
         self.params, self.opt, self.lib, self.device = list(params), opt, lib, device
@@ -572,7 +588,7 @@ class PPOTrainer:
             self._boot = (torch.empty((M, 6), dtype=torch.int8, device=self.device),
                           torch.empty((M,), dtype=torch.float32, device=self.device))
             self.fused.pack()
-            if _FUSED_ADAM and not any(g.get('weight_decay', 0) or g.get('amsgrad') for g in self.opt.param_groups):
+            if _FUSED_ADAM and FusedAdam.supports(self.opt):
                 self.fused_opt = FusedAdam(self.policy.parameters(), self.opt, self.fused.lib, self.device)
         else:
             self._sync_rollout_policy()

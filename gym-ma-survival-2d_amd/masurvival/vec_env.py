@@ -181,17 +181,17 @@ class VecMaSurvival:
 
     def force_general(self, on: bool = True, one_lane_solve: bool = False):
         """Test diagnostics: every env takes the general physics path (on);
-        one_lane_solve: the general path's Collide + Solve runs one lane per
-        env (k_gen_solve) instead of on lane groups (k_gen_solve_g)."""
+        one_lane_solve (test library libmas_ab.so only): the general path runs
+        the one-lane k_gen_solve + k_gen_toi instead of k_gen_solve_g."""
         bits = getattr(self, '_dbg_bits', 0) & 12
         self._dbg_bits = bits | int(bool(on)) | (2 if one_lane_solve else 0)
         check(self._lib.mas_debug_force_general(self._h, self._dbg_bits))
 
     def split_step(self, mode=None):
         """Test diagnostics: how mas_step uses the side stream (same results):
-        0 the caller's stream alone, 1 every general-path env on the side
-        stream, None the handle's default (the slow split, MAS_SPLIT)."""
-        bits = {0: 8, 1: 4, None: 0}[mode]
+        0 the caller's stream alone, None the handle's default (the slow
+        split, MAS_SPLIT)."""
+        bits = {0: 8, None: 0}[mode]
         self._dbg_bits = (getattr(self, '_dbg_bits', 0) & 3) | bits
         check(self._lib.mas_debug_force_general(self._h, self._dbg_bits))
 

@@ -288,26 +288,27 @@ int mas_policy_dw(int32_t f, int32_t g, int64_t k, const void* a, int64_t lda, c
 int mas_debug_counters(mas_handle* h, int64_t* host_out);
 
 /* Diagnostics (synchronises the device): host_out[0] = appends to the
- * general-path env list (and the optional SolveTOI list) that their bounds
- * refused since mas_create.  The lists hold one entry per env (per (env,
- * agent)) and are emptied every step, so this is 0 unless a kernel breaks
- * that invariant; the tests assert it. */
+ * general-path env list (and the slow list) that their bounds refused since
+ * mas_create.  The lists hold one entry per env and are emptied every step,
+ * so this is 0 unless a kernel breaks that invariant; the tests assert it. */
 int mas_debug_guards(mas_handle* h, int64_t* host_out);
 
 /* Test diagnostics: bit 0 of `on` sends every env of every following
  * mas_step through the general physics path (the contact-free fast path
- * gives up for all envs); bit 1 runs the general path's Collide + Solve one
- * lane per env (k_gen_solve) instead of on lane groups (k_gen_solve_g);
- * bits 2 and 3 pick how mas_step uses the handle's side stream.  Default
- * (MAS_SPLIT=2 in the environment at mas_create, or unset): the slow split,
- * the envs whose last general-path step had a SolveTOI at the sub-step cap
- * (or >= MAS_SLOW_K, default 4, TOI events) run their general path and post
- * phases on the side stream while the caller's stream runs the rest; it is
- * on for 8 steps after the general kernels last flagged such an env (a
- * host-mapped signal), else mas_step runs on one stream.  Bit 2
- * (or MAS_SPLIT=1): every general-path env on the side stream.  Bit 3 (or
- * MAS_SPLIT=0): the caller's stream alone.  Results are unchanged (every path
- * is exact): A/B and parity tests only. */
+ * gives up for all envs); bit 1 runs the general path one lane per env
+ * (k_gen_solve + k_gen_toi) instead of on lane groups (k_gen_solve_g) -- only
+ * in the test library libmas_ab.so (`make ab`), MAS_ERR_UNSUPPORTED here;
+ * bit 3 keeps mas_step on the caller's stream.  Default (MAS_SPLIT unset or
+ * 2 in the environment at mas_create): the slow split, the envs whose last
+ * general-path step had a SolveTOI at the sub-step cap (or >= MAS_SLOW_K,
+ * default 4, TOI events) run their general path and post phases on the side
+ * stream while the caller's stream runs the rest; it is on for 8 steps after
+ * the general kernels last flagged such an env (a host-mapped signal), else
+ * mas_step runs on one stream.  Bit 3 (or MAS_SPLIT=0): the caller's stream
+ * alone -- the form a caller may capture into a graph and replay (the
+ * general-path list is emptied on the device).  Bit 2 (the former
+ * all-general split) is rejected with MAS_ERR_INVALID_ARG.  Results are
+ * unchanged (every path is exact): A/B and parity tests only. */
 int mas_debug_force_general(mas_handle* h, int32_t on);
 
 /* Action validation.  The reference asserts action_space.contains(actions)

@@ -26,7 +26,7 @@ def per_step(path, counter, last):
     steps = []
     for r in rows:
         k = r['Kernel_Name'].split('<')[0].replace('void mas::', '')
-        if k == 'k_pre':
+        if k in ('k_pre', 'k_pre_lanes'):
             steps.append(collections.defaultdict(float))
         if not steps or k in ('k_seed', 'k_stats'):
             continue

@@ -18,7 +18,7 @@ def main(path, steps=20):
         disp[d][r['Counter_Name']] = disp[d].get(r['Counter_Name'], 0.0) + float(r['Counter_Value'])
         names[d] = r['Kernel_Name'].split('<')[0].replace('void mas::', '')
     order = sorted(disp)
-    starts = [d for d in order if names[d] == 'k_pre']
+    starts = [d for d in order if names[d] in ('k_pre', 'k_pre_lanes')]
     keep = set(d for d in order if d >= starts[-steps]) if len(starts) >= steps else set(order)
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for d in keep:

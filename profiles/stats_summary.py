@@ -16,7 +16,7 @@ def step_spans(trace):
     spans, t0, t1 = [], None, None
     for r in rows:
         n = r['Kernel_Name']
-        if 'mas::k_pre<' in n:
+        if 'mas::k_pre<' in n or 'mas::k_pre_lanes<' in n:
             if t0 is not None and t1 is not None:
                 spans.append((t1 - t0) / 1e6)
             t0, t1 = int(r['Start_Timestamp']), None

@@ -1,7 +1,8 @@
 """A/B of the general path's Collide + Solve kernels on a golden episode:
 two n_envs = 1 handles replay the fixture's actions in lockstep, one with the
-lane-group k_gen_solve_g (default), one with the one-lane k_gen_solve
-(mas_debug_force_general bit 1).  After every step their mas_get_state
+lane-group k_gen_solve_g (default), one with the one-lane k_gen_solve +
+k_gen_toi (mas_debug_force_general bit 1; these kernels are only in the test
+library libmas_ab.so, `make -C gym-ma-survival-2d_amd/csrc ab`).  After every step their mas_get_state
 images are compared; at the first difference the differing words (index,
 both values) and the step are printed and both images are saved.
 usage: python scripts/ab_solve_golden.py <fixture.npz> [out.npz]"""
@@ -10,6 +11,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'gym-ma-survival-2d_amd'))
+# the one-lane kernels live only in the test build (make -C .../csrc ab)
+os.environ.setdefault('MAS_LIB', os.path.join(ROOT, 'gym-ma-survival-2d_amd', 'masurvival', '_lib', 'libmas_ab.so'))
 sys.path.insert(0, os.path.join(ROOT, 'tests'))
 
 import numpy as np  # noqa: E402

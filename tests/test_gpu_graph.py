@@ -1,0 +1,67 @@
+"""A graph-captured mas_step replays like eager steps (INTEGRATION.md
+"Graph capture").
+
+With the handle on one stream (MAS_SPLIT=0 / mas_debug_force_general bit 3)
+mas_step keeps no host state between calls: the general-path list count is
+zeroed on the device by the first post kernel after its last reader.  One
+handle steps eagerly, a second replays a HIP graph of one captured step with
+the same actions copied into its static action buffer; obs, rewards, done,
+the general-path counts and the final state images must be identical, and no
+list append may be refused (a count that grew across replays would re-step
+stale entries and then overflow the list)."""
+import pytest
+
+torch = pytest.importorskip('torch')
+pytestmark = pytest.mark.gpu
+
+from masurvival import abi  # noqa: E402
+from masurvival.config import C3_CONFIG, C5_CONFIG  # noqa: E402
+from masurvival.vec_env import VecMaSurvival  # noqa: E402
+
+HI = torch.tensor([3, 3, 3, 2, 2, 2])
+
+
+@pytest.mark.parametrize('name,cfg,n,T,forced', [
+    ('C3 2v2', C3_CONFIG, 4096, 120, False),
+    ('C3 2v2 forced general', C3_CONFIG, 2048, 40, True),
+    ('C5 ffa4', C5_CONFIG, 1024, 80, False)])
+def test_captured_step_replays_like_eager(name, cfg, n, T, forced):
+    try:
+        eager = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
+        graph = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
+    except abi.MasError as e:
+        if 'no compiled capacity class' in str(e):
+            pytest.skip(str(e))
+        raise
+    for e in (eager, graph):
+        e.split_step(0)
+        if forced:
+            e.force_general(True)
+    assert torch.equal(eager.reset(), graph.reset())
+    act = torch.zeros((n, graph.n_agents, 6), dtype=torch.int8, device=graph.device)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        graph.step(act)
+    gen = torch.Generator(device=graph.device)
+    gen.manual_seed(n + 17)
+    hi = HI.to(graph.device)
+    general = 0
+    for t in range(T):
+        a = (torch.rand((n, graph.n_agents, 6), generator=gen, device=graph.device) * hi).to(torch.int8)
+        act.copy_(a)
+        g.replay()
+        o1, r1, d1, _ = eager.step(a)
+        assert torch.equal(d1, graph.dones), (name, t)
+        assert torch.equal(r1, graph.rewards), (name, t)
+        assert torch.equal(o1, graph.obs), (name, t)
+        c1, c2 = eager.debug_counters()['phys_general_envs'], graph.debug_counters()['phys_general_envs']
+        assert c1 == c2, (name, t, c1, c2)
+        general += c1
+    assert general > 0
+    assert torch.equal(eager.get_state(), graph.get_state())
+    assert eager.debug_guards()['list_overflow'] == 0
+    assert graph.debug_guards()['list_overflow'] == 0
+    del g
+    eager.close()
+    graph.close()

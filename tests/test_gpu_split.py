@@ -1,16 +1,12 @@
-"""The split steps against the one-stream order (mas_debug_force_general
-bits 2 / 3, MAS_SPLIT): two handles on the same seeds and actions must give
+"""The slow split against the one-stream order (mas_debug_force_general
+bit 3, MAS_SPLIT): two handles on the same seeds and actions must give
 bit-identical obs, rewards, done flags and state images, with auto-reset.
 
-- mode 1: every general-path env runs its general path and its k_cameras /
-  k_post / k_obs on the handle's side stream, the other envs' on the
-  caller's stream;
-- the default, the slow split: only the envs whose previous general-path
-  step was slow (a SolveTOI at the sub-step cap, or >= MAS_SLOW_K TOI
-  events) go to the side stream.  MAS_SLOW_K=1 here, so that every env with
-  a TOI event the step before takes the side stream and the slow list is
-  busy at these sizes (the product default, 4, picks the few wedged envs of
-  the PPO regime).
+In the slow split only the envs whose previous general-path step was slow
+(a SolveTOI at the sub-step cap, or >= MAS_SLOW_K TOI events) go to the
+side stream.  MAS_SLOW_K=1 here, so that every env with a TOI event the step
+before takes the side stream and the slow list is busy at these sizes (the
+product default, 4, picks the few wedged envs of the PPO regime).
 
 The contact-heavy regime is random actions (plus every env forced onto the
 general path in one case: the list-mode kernels then run every env)."""
@@ -38,9 +34,7 @@ LID_2V2 = {'agents': {'n_agents': 4, 'agent_size': 1}, 'teams': {'twoteams': Tru
     ('C5 ffa4 slow', C5_CONFIG, 2048, 200, None, False, True),
     ('C3 2v2 slow forced', C3_CONFIG, 4096, 60, None, True, True),
     ('C3 2v2 slow no auto-reset', C3_CONFIG, 4096, 160, None, False, False),
-    ('2v2 lidars slow', LID_2V2, 4096, 160, None, False, True),
-    ('C3 2v2 all', C3_CONFIG, 8192, 120, 1, False, True),
-    ('C3 2v2 all forced', C3_CONFIG, 4096, 40, 1, True, True)])
+    ('2v2 lidars slow', LID_2V2, 4096, 160, None, False, True)])
 def test_split_step_matches_one_stream(name, cfg, n, T, mode, forced, ar, monkeypatch):
     monkeypatch.setenv('MAS_SLOW_K', '1')
     monkeypatch.delenv('MAS_SPLIT', raising=False)

@@ -164,3 +164,18 @@ def test_checkpoint_resume_continues_the_same_trajectory(tmp_path):
         assert torch.equal(s1[k]['exp_avg'], s2[k]['exp_avg'])
         assert torch.equal(s1[k]['exp_avg_sq'], s2[k]['exp_avg_sq'])
     assert torch.equal(tr.buf.obs[0], tr2.buf.obs[0]) and tr.steps_taken == tr2.steps_taken
+
+
+def test_fused_adam_only_for_plain_adam():
+    """FusedAdam restates clip + torch.optim.Adam for one plain param group
+    only; any other optimizer setup stays on torch."""
+    import torch
+    from masurvival.ppo import FusedAdam
+    w = [torch.nn.Parameter(torch.zeros(3)), torch.nn.Parameter(torch.zeros(2))]
+    assert FusedAdam.supports(torch.optim.Adam(w, lr=1e-3, eps=1e-5))
+    assert not FusedAdam.supports(torch.optim.Adam([{'params': w[:1]}, {'params': w[1:]}], lr=1e-3))
+    assert not FusedAdam.supports(torch.optim.Adam(w, lr=1e-3, maximize=True))
+    assert not FusedAdam.supports(torch.optim.Adam(w, lr=1e-3, weight_decay=0.1))
+    assert not FusedAdam.supports(torch.optim.Adam(w, lr=1e-3, amsgrad=True))
+    assert not FusedAdam.supports(torch.optim.Adam(w, lr=torch.tensor(1e-3)))
+    assert not FusedAdam.supports(torch.optim.SGD(w, lr=1e-3))
