@@ -336,11 +336,16 @@ __device__ __forceinline__ bool world_step_fast_lane(AgentL<C>& g, bool alive, b
     return env_ballot<C>(bail) == 0u;
 }
 
+// waves per SIMD the register budget of k_pre_lanes allows (4: 128 VGPRs, a
+// 12-register spill for 2v2; 3: 168, none)
+#ifndef MAS_PRE_OCC
+#define MAS_PRE_OCC 4
+#endif
 // k_pre on agent lanes: queue_actions, Object drops, DynamicMotors, UseLast,
 // GiveLast, Melee (step_pre order), the dirty stores, then the speculative
 // contact-free 2 x world.Step and the general-path list append (fast_phys).
 template <class C>
-__global__ __launch_bounds__(kWG, 4) void k_pre_lanes(Params P, uint32_t* __restrict__ state, int64_t N,
+__global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32_t* __restrict__ state, int64_t N,
                                                       const int8_t* __restrict__ actions)
 {
     using LY = Lay<C>;

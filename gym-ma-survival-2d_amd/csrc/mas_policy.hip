@@ -47,12 +47,7 @@ constexpr float kTanhC = 2.8853900817779268f;  // 2 log2(e)
 #define MAS_POL_WAVES 4
 #endif
 constexpr int kWaves = MAS_POL_WAVES;  // waves per workgroup (4: one per SIMD, two workgroups per CU)
-// waves per workgroup of the train kernel (a value other than kWaves needs the
-// double-buffered stages, MAS_POL_DB, whose copy loop is sized by it)
-#ifndef MAS_POL_TWAVES
-#define MAS_POL_TWAVES MAS_POL_WAVES
-#endif
-constexpr int kTWaves = MAS_POL_TWAVES;
+constexpr int kTWaves = kWaves;  // waves per workgroup of the train kernel
 constexpr int kLdsFrag = 4608;  // 72 KiB LDS weight stage (16-B fragments): two workgroups per CU
 constexpr int kKc = kLdsFrag / (kMT * 64);  // layer-1 k-steps per stage (9)
 constexpr int kHalf = kMT / 2 * 16 + 8;     // fragment slots of one forward half stage: W2 4 M-tiles + W3 8 k-steps
@@ -277,73 +272,6 @@ struct Stage1 {
     }
 };
 
-// MAS_POL_DB (train kernel): two buffers; stage i + 1's LDS-DMA is issued
-// right after the barrier that opens stage i, so it lands while the waves
-// compute from stage i.  The stage list is the train kernel's fixed order
-// (stage_src): W1 chunks, the two forward halves, W3^T, the two W2^T halves.
-#ifndef MAS_POL_DB
-#define MAS_POL_DB 0
-#endif
-static_assert(MAS_POL_DB || kTWaves == kWaves, "a train workgroup size of its own needs MAS_POL_DB");
-constexpr int kTStagePer = kLdsFrag / (64 * kTWaves);
-__device__ __forceinline__ void stage_issue(bf8* __restrict__ wl, const bf8* __restrict__ src, int n)
-{
-    const int w0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
-    const uint32_t loff = (threadIdx.x & 63) * 16u;
-#pragma unroll
-    for (int k = 0; k < kTStagePer; ++k) {
-        const int i0 = w0 + k * 64 * kTWaves;
-        if (i0 < n)  // wave-uniform
-            __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint8_t*>(src + i0) + loff),
-                                             (lds_void*)(wl + i0), 16, 0, 0);
-    }
-}
-struct Stage2 {
-    bf8* wl;  // 2 x kLdsFrag
-    const bf8* F;
-    int64_t w1, w23, wbk;
-    int ks1, nw1, i;
-    __device__ __forceinline__ const bf8* src(int j, int& n) const
-    {
-        if (j < nw1) {
-            const int k0 = j * kKc, kn = ks1 - k0 < kKc ? ks1 - k0 : kKc;
-            n = kn * kMT * 64;
-            return F + w1 + (int64_t)k0 * kMT * 64;
-        }
-        j -= nw1;
-        if (j < 2) {
-            n = kHalf * 64;
-            return F + w23 + j * kHalf * 64;
-        }
-        j -= 2;
-        if (j == 0) {
-            n = kBk0 * 64;
-            return F + wbk;
-        }
-        n = kBk1 * 64;
-        return F + wbk + (kBk0 + (j - 1) * kBk1) * 64;
-    }
-    __device__ __forceinline__ void prime()
-    {
-        int n;
-        const bf8* s0 = src(0, n);
-        __syncthreads();
-        stage_issue(wl, s0, n);
-    }
-    __device__ __forceinline__ const bf8* operator()(const bf8*, int)
-    {
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's copy of stage i landed
-        __syncthreads();                // every wave's copy landed; stage i - 1 free
-        if (i + 1 < nw1 + 5) {
-            int n;
-            const bf8* s1 = src(i + 1, n);
-            stage_issue(wl + ((i + 1) & 1) * kLdsFrag, s1, n);
-        }
-        const bf8* r = wl + (i & 1) * kLdsFrag;
-        ++i;
-        return r;
-    }
-};
 
 __device__ __forceinline__ void tanh_h1(const f16v (&acc)[kMT], const float* __restrict__ b1p, int h,
                                         bf8 (&h1)[kMT][2])
@@ -679,14 +607,8 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
     const Layout Lo{A.ks1};
     const bf8* F = reinterpret_cast<const bf8*>(A.packed);
     const float* FB = reinterpret_cast<const float*>(A.packed);
-#if MAS_POL_DB
-    __shared__ bf8 wl[2 * kLdsFrag];
-    Stage2 S{wl, F, Lo.w1(), Lo.w23(), Lo.wbk(), A.ks1, (A.ks1 + kKc - 1) / kKc, 0};
-    S.prime();
-#else
     __shared__ bf8 wl[kLdsFrag];
     Stage1 S{wl};
-#endif
     const int l = threadIdx.x & 63, h = l >> 5, wv = threadIdx.x >> 6;
     const int64_t M = A.M, LD = A.ld;
     const int64_t row0 = ((int64_t)blockIdx.x * kTWaves + wv) * 32;

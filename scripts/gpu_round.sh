@@ -38,6 +38,13 @@ for step in "$@"; do
       cd $R && timeout -k 10 200 python bench.py --mode env --no-cpu-baseline > $O/bench_env.log 2>&1 || exit $?
       cd $R && timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_ffa.log 2>&1 || exit $?
       cd $R && timeout -k 10 200 python bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline > $O/bench_1v1.log 2>&1 || exit $? ;;
+    full)
+      # the C4 / C5 workloads at their configured env counts on one GPU
+      cd $R && timeout -k 10 300 python bench.py --mode env --envs 262144 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_env_c4full.log 2>&1 || exit $?
+      cd $R && timeout -k 10 300 python bench.py --mode env --config ffa4 --envs 131072 --steps 30 --warmup 10 --no-cpu-baseline > $O/bench_env_c5full.log 2>&1 || exit $? ;;
+    envprof2)
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_env -o run -- \
+        python3 $R/bench.py --mode env --no-cpu-baseline > $O/prof_env.log 2>&1 || exit $? ;;
     prof)
       cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- \
         python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.log 2>&1 || exit $?
