@@ -352,6 +352,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
     constexpr int S = kWG / C::AM, AM = C::AM;
     static_assert(kWG % AM == 0 && (AM & (AM - 1)) == 0, "agent lane groups must tile a wave");
     __shared__ PreLds<C> lds;
+    MAS_PROF(P, -1);
     const int lane = (int)threadIdx.x;
     const int j = lane / AM, i = lane - j * AM;
     const int64_t e0 = (int64_t)blockIdx.x * S, e = e0 + j;
@@ -425,6 +426,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
     lds.ax[i * S + j] = g.c.x;
     lds.ay[i * S + j] = g.c.y;
     wave_lds_sync();  // the wave's LDS groups are loaded (one-wave block)
+    MAS_PROF(P, 20);
     uint32_t dirty = kGDyn;
     // ---------------- pre_step ----------------
     // boxes: Object.pre_step drops last step's queued box items
@@ -549,6 +551,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
         }
         if (gave_any) dirty |= kGRule;
     }
+    MAS_PROF(P, 21);
     // Melee / ContinuousMelee (semantics.py:531-554, 584-610): every ray
     // first (each lane casts its own agent's), then the attacks in agent
     // order; the cooldowns are those the attack loop sees
@@ -591,6 +594,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
             dirty |= kGRule;
         }
     }
+    MAS_PROF(P, 22);
     // ---------------- stores: only the groups this step changed ----------------
     // (step_pre's dirty mask, ORed over the env's agents)
     uint32_t dirty_env = dirty;
@@ -642,6 +646,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
         if (si) group_store<S>(lds.item, state, N, e0, LY::item, LY::kItemW, si);
         if (sp) group_store<S>(lds.pend, state, N, e0, LY::pend, LY::kItemW, sp);
     }
+    MAS_PROF(P, 23);
     // ---------------- speculative contact-free physics (fast_phys) ----------------
     bool ok = touch_w == 0u;
     ok = env_ballot<C>(!ok) == 0u && !P.force_general;
@@ -662,6 +667,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
             }
         }
     }
+    MAS_PROF(P, 24);
     // the general-path list append and the slow routing, one lane per env
     const bool lead = i == 0 && valid;
     bool slow = false;
@@ -687,6 +693,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
             else atomicAdd(P.list_overflow, 1);
         }
     }
+    MAS_PROF(P, 25);
 }
 
 }  // namespace mas

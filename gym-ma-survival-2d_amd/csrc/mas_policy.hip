@@ -799,6 +799,279 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
 
 
 // ---------------------------------------------------------------------------
+// k_policy_train_cw: k_policy_train's feature-major pair-store path (the PPO
+// update's: M and ld even, not row-major) with the activation stores moved
+// off the weight-stage drains.  vmcnt counts loads, stores and LDS-DMA
+// together in issue order, so stage()'s wait for the stage's LDS-DMA copies
+// (s_waitcnt 0) also waited for every activation store the wave had issued
+// before them: each of the six stage boundaries of a block drained the
+// block's stores with the wave parked at the barrier.  Here each boundary
+// issues the next stage's copies first and only then the stores of values
+// the previous phase finished (kept in registers until then: h1, h2, dA2,
+// half of dA1), and waits with vmcnt(n) for n <= the stores issued after the
+// copies -- the copies are older than those stores, so they have landed --
+// leaving the stores in flight through the next phase's MFMAs.  Same values,
+// same addresses: only the issue order of the stores moves.
+// ---------------------------------------------------------------------------
+// dA2 M-tiles stored behind the first W2^T copies (8 stores each; more than
+// two spill: the scheduler hoists the stage's LDS reads above the stores)
+#ifndef MAS_POL_CW_DEFER
+#define MAS_POL_CW_DEFER 3
+#endif
+// dA1 M-tiles of the first W2^T half stored behind the second half's copies
+#ifndef MAS_POL_CW_DEFER1
+#define MAS_POL_CW_DEFER1 3
+#endif
+// a bare workgroup barrier: __syncthreads()'s workgroup-scope fences (even
+// restricted to LDS: the LDS-DMA copies are LDS writes counted by vmcnt) make
+// the compiler wait vmcnt(0) for the wave's outstanding stores -- the drain
+// this kernel exists to avoid.  The ordering they gave is explicit here: the
+// callers' s_waitcnt retires the wave's LDS traffic and copies, and the empty
+// asm statements keep the compiler from moving memory accesses across.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_s_waitcnt((0x3F & 0xF) | ((0x3F >> 4) << 14) | (0x7 << 4) | (0 << 8));  // lgkmcnt(0)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+// LDS-DMA copy of a stage of N fragments (no wait): stage() without its
+// drain.  N is a multiple of the workgroup's 64 kWaves lanes, so every wave
+// issues the same N / (64 kWaves) copies: no wave-dependent branch, which
+// would give the compiler's wait-count analysis a path without copies
+template <int N>
+__device__ __forceinline__ void stage_copy(bf8* __restrict__ wl, const bf8* __restrict__ src)
+{
+    static_assert(N % (64 * kWaves) == 0 && N <= kLdsFrag, "whole copy rounds");
+    lds_barrier();  // every wave is done with the previous stage
+    const int w0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+    const uint32_t loff = (threadIdx.x & 63) * 16u;
+#pragma unroll
+    for (int k = 0; k < N / (64 * kWaves); ++k) {
+        const int i0 = w0 + k * 64 * kWaves;
+        __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint8_t*>(src + i0) + loff),
+                                         (lds_void*)(wl + i0), 16, 0, 0);
+    }
+}
+// the stage's copies have landed once at most NST of the wave's vector memory
+// operations are outstanding, NST <= the stores issued after the copies (a
+// wave without rows issued none: it waits for everything)
+template <int NST>
+__device__ __forceinline__ void stage_landed(bool issued)
+{
+    static_assert(NST >= 0 && NST <= 63, "vmcnt is 6 bits");
+    // gfx9 s_waitcnt: vmcnt [3:0] + [15:14], expcnt [6:4] and lgkmcnt [11:8] at their maximum (no wait)
+    constexpr int imm = (NST & 0xF) | ((NST >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+    if (issued) __builtin_amdgcn_s_waitcnt(imm);
+    else __builtin_amdgcn_s_waitcnt(0);
+    lds_barrier();  // every wave's copies have landed
+}
+
+// one block's rows; FULL: every row of the block is in range (all blocks
+// but the last), so no store sits under a branch -- a path that skips stores
+// would leave the copies the newest operations and force vmcnt(0) waits
+template <int KS, bool OFF32, bool FULL>
+__device__ __forceinline__ void train_cw_block(const TrainArgs& A, bf8* wl, float (&st)[4])
+{
+    const Layout Lo{A.ks1};
+    const bf8* F = reinterpret_cast<const bf8*>(A.packed);
+    const float* FB = reinterpret_cast<const float*>(A.packed);
+    Stage1 S{wl};
+    const int l = threadIdx.x & 63, h = l >> 5, wv = threadIdx.x >> 6;
+    const int64_t M = A.M, LD = A.ld;
+    const int64_t row0 = ((int64_t)blockIdx.x * kTWaves + wv) * 32;
+    const int64_t row = row0 + (l & 31);
+    const bool ok = FULL || row < M;
+    const bool on = FULL || row0 < M;  // wave-uniform: the wave has rows (its stores are issued)
+    // (M even: both rows of a lane pair are in range or neither)
+    {
+        bf8 h1[kMT][2], h2[kMT][2];
+        const int64_t rr = ok ? row : M - 1;
+        auto xf = [&](int ks) { return *reinterpret_cast<const bf8*>(A.xb + rr * A.xb_stride + 16 * ks + 8 * h); };
+        if constexpr (KS > 0) {
+            bf8 x[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) x[ks] = xf(ks);
+            layer1_reg<KS>(S, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
+        } else {
+            layer1(S, F + Lo.w1(), FB + Lo.b1(), A.ks1, l, on, xf, h1);
+        }
+        auto st2 = [&](__bf16* base, int t, const bf8 (&v)[2]) {
+            if (ok) store_rows2<OFF32>(base, LD, row, t, h, v);
+        };
+        const f16v z3 = layers23<true>(S, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);
+        // the loss inputs of this row, loaded ahead of the activation stores
+        // (a load issued after them would wait for them: vmcnt is in order);
+        // the output biases through the scalar cache
+        const int64_t rl = ok ? row : M - 1;
+        const uint16_t* ap = reinterpret_cast<const uint16_t*>(A.act + rl * 6);  // 2-byte aligned
+        const uint32_t a01 = ap[0], a23 = ap[1], a45 = ap[2];
+        const float adv = A.adv[rl], old_lp = A.old_logp[rl], ret = A.ret[rl];
+        typedef const __attribute__((address_space(4))) float cfloat;
+        const cfloat* b3 = (const cfloat*)(FB + Lo.b3());
+        // W3^T; h1 and h2 go out behind its copies
+        stage_copy<kBk0 * 64>(wl, F + Lo.wbk());
+        if (on) {
+#pragma unroll
+            for (int mt = 0; mt < kMT; ++mt) {  // 128 stores
+                st2(A.h1, mt, h1[mt]);
+                st2(A.h2, mt, h2[mt]);
+            }
+        }
+        stage_landed<63>(on);
+        const bf8* wb = wl;
+        // PPO loss gradient of this row (lane half 0 holds the 16 outputs)
+        float dz[kO];
+#pragma unroll
+        for (int o = 0; o < kO; ++o) dz[o] = 0.0f;
+        if (on && h == 0 && ok) {
+            float z[kO];
+#pragma unroll
+            for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
+            int a[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) a[k] = (int)(int8_t)(((k < 2 ? a01 : k < 4 ? a23 : a45) >> (8 * (k & 1))) & 0xffu);
+            float lsm[15], p[15], hent[6];
+            float lp = 0.0f, ent = 0.0f;
+#pragma unroll
+            for (int hd = 0; hd < 6; ++hd) {
+                const int n = kHeadN[hd], off = kHeadOff[hd];
+                float mx = z[off];
+#pragma unroll
+                for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
+                float se = 0.0f;
+#pragma unroll
+                for (int k = 0; k < n; ++k) se += exp_fast(z[off + k] - mx);
+                const float lse = mx + log_fast(se);
+                float e = 0.0f;
+                const int ak = a[hd];
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    lsm[off + k] = z[off + k] - lse;
+                    p[off + k] = exp_fast(lsm[off + k]);
+                    e -= p[off + k] * lsm[off + k];
+                    if (k == ak) lp += lsm[off + k];
+                }
+                hent[hd] = e;
+                ent += e;
+            }
+            const float ratio = exp_fast(lp - old_lp);
+            const float s1 = ratio * adv;
+            const float rc = fminf(fmaxf(ratio, 1.0f - A.clip), 1.0f + A.clip);
+            const float s2 = rc * adv;
+            const float glp = s1 <= s2 ? -s1 : 0.0f;
+            const float sc = A.scale;
+#pragma unroll
+            for (int hd = 0; hd < 6; ++hd) {
+                const int n = kHeadN[hd], off = kHeadOff[hd];
+                const int ak = a[hd];
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    const float oh = k == ak ? 1.0f : 0.0f;
+                    dz[off + k] = sc * (glp * (oh - p[off + k]) + A.ent_coef * p[off + k] * (lsm[off + k] + hent[hd]));
+                }
+            }
+            const float dv = z[kO - 1] - ret;
+            dz[kO - 1] = sc * A.vf_coef * 2.0f * dv;
+            st[0] = -fminf(s1, s2);
+            st[1] = dv * dv;
+            st[2] = ent;
+            st[3] = fabsf(ratio - 1.0f) > A.clip ? 1.0f : 0.0f;
+#pragma unroll
+            for (int o = 0; o < kO; ++o) A.dz[(int64_t)o * LD + row] = (__bf16)dz[o];
+        }
+        bf8 dzf[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dzf[i >> 3][i & 7] = (__bf16)dz[i];
+        // dA2 = (W3^T dz) * (1 - h2^2), by M-tile of layer 2 (kept in registers)
+        bf8 da2[kMT][2];
+        const bf8* W3T = wb + l;
+#pragma unroll
+        for (int mo = 0; mo < kMT; ++mo) {
+            f16v g = f16v{};
+            g = mfma(W3T[(mo * 2) * 64], dzf[0], g);
+            g = mfma(W3T[(mo * 2 + 1) * 64], dzf[1], g);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float hv = (float)h2[mo][i >> 3][i & 7];
+                da2[mo][i >> 3][i & 7] = (__bf16)(g[i] * dtanh(hv));
+            }
+            if (on && mo < kMT - MAS_POL_CW_DEFER) st2(A.da2, mo, da2[mo]);
+        }
+        // dA1 = (W2^T dA2) * (1 - h1^2), by M-tile of layer 1, in two half
+        // stages; dA2 goes out behind the first half's copies (dA1 is stored
+        // as computed: holding tiles 0..3 for the second boundary would spill)
+        const bf8* W2T = nullptr;
+        bf8 d1k[kMT / 2][2];  // the deferred tiles (MAS_POL_CW_DEFER1 of them)
+#pragma unroll
+        for (int mt = 0; mt < kMT; ++mt) {
+            if (mt == 0) {
+                stage_copy<kBk1 * 64>(wl, F + Lo.wbk() + kBk0 * 64);
+                if (on) {
+#pragma unroll
+                    for (int mo = kMT - MAS_POL_CW_DEFER; mo < kMT; ++mo) st2(A.da2, mo, da2[mo]);
+                }
+                stage_landed<8 * MAS_POL_CW_DEFER>(on);
+                W2T = wl + l;
+            } else if (mt == kMT / 2) {
+                stage_copy<kBk1 * 64>(wl, F + Lo.wbk() + (kBk0 + kBk1) * 64);
+                if (on) {
+#pragma unroll
+                    for (int q = kMT / 2 - MAS_POL_CW_DEFER1; q < kMT / 2; ++q) st2(A.da1, q, d1k[q]);
+                }
+                stage_landed<8 * MAS_POL_CW_DEFER1>(on);
+                W2T = wl + l;
+            }
+            f16v g = f16v{};
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) g = mfma(W2T[((mt % (kMT / 2)) * 16 + kk) * 64], da2[kk >> 1][kk & 1], g);
+            bf8 d1[2];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float hv = (float)h1[mt][i >> 3][i & 7];
+                d1[i >> 3][i & 7] = (__bf16)(g[i] * dtanh(hv));
+            }
+            if (mt >= kMT / 2 - MAS_POL_CW_DEFER1 && mt < kMT / 2) {
+                d1k[mt][0] = d1[0];
+                d1k[mt][1] = d1[1];
+            } else if (on) {
+                st2(A.da1, mt, d1);
+            }
+        }
+    }
+}
+
+template <int KS, bool OFF32>
+__global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_policy_train_cw(TrainArgs A)
+{
+    __shared__ bf8 wl[kLdsFrag];
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if ((int64_t)(blockIdx.x + 1) * kTWaves * 32 <= A.M)  // block-uniform
+        train_cw_block<KS, OFF32, true>(A, wl, st);
+    else
+        train_cw_block<KS, OFF32, false>(A, wl, st);
+
+    // per-block loss partials (through the LDS stage, after its last reader)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(wl);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float v = st[k];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (l == 0) red[wv * 4 + k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kTWaves; ++w) v += red[w * 4 + threadIdx.x];
+        A.partials[(int64_t)blockIdx.x * 4 + threadIdx.x] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradients of one minibatch, dW = A B^T and db = row sums of A, over
 // the minibatch rows K: A [F][K] (dA2 or dz) and B [G][K] (h1 or h2) are the
 // feature-major bf16 activations mas_policy_train writes (K contiguous, row
@@ -1213,6 +1486,16 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     // offsets that only buffers over 4 GB take, on any size
     const char* f64 = getenv("MAS_POL_FORCE_OFF64");
     const bool o32 = ld <= pol::kOff32Ld && !(f64 && f64[0] == '1');
+    // the counted-wait kernel for the PPO update's store mode (feature-major,
+    // two rows per lane: M and ld even) with 32-bit store offsets; its 64-bit
+    // offset and 9-k-step layer-1 builds spill (compiler resource report), so
+    // those keep k_policy_train.  MAS_POL_CW=0: k_policy_train everywhere
+    const char* cw = getenv("MAS_POL_CW");
+    if (!rm && o32 && A.ks1 != 9 && ((M | ld) & 1) == 0 && !(cw && cw[0] == '0')) {
+        auto kc = A.ks1 == 10 ? pol::k_policy_train_cw<10, true> : pol::k_policy_train_cw<0, true>;
+        hipLaunchKernelGGL(kc, dim3((unsigned)policy_blocks(M)), dim3(64 * pol::kTWaves), 0, s, A);
+        return hipGetLastError();
+    }
     auto k = rm ? (A.ks1 == 10 ? pol::k_policy_train<10, false, true>
                    : A.ks1 == 9 ? pol::k_policy_train<9, false, true> : pol::k_policy_train<0, false, true>)
            : A.ks1 == 10 ? (o32 ? pol::k_policy_train<10, true, false> : pol::k_policy_train<10, false, false>)

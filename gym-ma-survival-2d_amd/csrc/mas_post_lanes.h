@@ -472,6 +472,7 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
     static_assert(kWG % AM == 0 && (AM & (AM - 1)) == 0, "agent lane groups must tile a wave");
     static_assert(C::NB <= 64 && AM <= 8, "16-bit camera list entries, 64-bit body masks");
     __shared__ PostLds<C> lds;
+    MAS_PROF(P, -1);
     retire_phys_count<M>(P);
     const int lane = (int)threadIdx.x;
     const int j = lane / AM, i = lane - j * AM;
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
     V.ag(4, i) = g.v.y;
     V.ag(5, i) = g.w;
     wave_lds_sync();  // the wave's LDS groups are loaded (one-wave block)
-    MAS_PROF(P, 34);
+    MAS_PROF(P, 41);
     // ---- boxes: Health.post_step + despawn (the first post_step hook, dict
     // order: the boxes group before the agents)
     bool bchanged = false;
@@ -613,7 +614,7 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
         }
         wave_lds_sync();  // the seen rows are complete
     }
-    MAS_PROF(P, 35);
+    MAS_PROF(P, 42);
     // ---------------- agents post_step (step_post, mas_step.h) ----------------
     uint32_t dirty = kGZone | kGStat;
     // Health.post_step -> despawn dead (id order): TrackDeaths, IndexBodies,
@@ -880,7 +881,7 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
             st[state_index(LY::stat + 16, e, N)] += 1.0f;
         }
     }
-    MAS_PROF(P, 36);
+    MAS_PROF(P, 43);
     // ---------------- stores: the groups this step changed ----------------
     uint32_t dirty_env = dirty;
 #pragma unroll
@@ -941,7 +942,7 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
             }
         }
     }
-    MAS_PROF(P, 37);
+    MAS_PROF(P, 44);
     // ---------------- fetch_observations: rows from LDS ----------------
     V.ag(6, i) = (float)g.health;
     int lastmeta = 0;
@@ -965,22 +966,34 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
             write_obs_row_v(V, P, alive_m, i, lastmeta, lhx, lhy, sink);
         }
         wave_lds_sync();  // the tile's rows are in LDS
-        // lane = (row half, column): rows q and q + 1 per instruction pair
+        // lane = (row parity, column): each store instruction writes two
+        // 128-B row segments; 8 rows per lane per chunk, the LDS reads of a
+        // chunk issued before its stores
         const int col = lane & (kPostObsW - 1), half = lane / kPostObsW;
         const bool col_ok = c0 + col < D;
-        for (int q = half; q < kWG; q += 2) {
-            if (q >= S * A) break;
-            // tile row q: slot q / A, agent q % A
-            const int sq = q / A, aq = q - sq * A;
-            const bool on = (act >> (sq * AM + aq)) & 1ull;
-            if (!on || !col_ok) continue;
-            const int64_t orow = M == kGenEnvs ? lds.eidx[sq] * A + aq : r0 + q;
-            obs[orow * D + c0 + col] = lds.u.tile[q * (kPostObsW + 1) + col];
+        const int nrows = S * A;
+        for (int q0 = 0; q0 < nrows; q0 += 16) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int q = q0 + 2 * k + half;
+                v[k] = q < nrows ? lds.u.tile[q * (kPostObsW + 1) + col] : 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int q = q0 + 2 * k + half;
+                const int sq = q / A, aq = q - sq * A;  // tile row q: slot q / A, agent q % A
+                const bool on = q < nrows && ((act >> (sq * AM + aq)) & 1ull);
+                if (on && col_ok) {
+                    const int64_t orow = M == kGenEnvs ? lds.eidx[sq] * A + aq : r0 + q;
+                    obs[orow * D + c0 + col] = v[k];
+                }
+            }
         }
         wave_lds_sync();  // the tile's reads are done before the next window's rows
     }
     (void)rr;
-    MAS_PROF(P, 38);
+    MAS_PROF(P, 45);
 }
 
 }  // namespace mas

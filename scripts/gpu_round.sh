@@ -28,6 +28,9 @@ for step in "$@"; do
     bench)
       cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_driver.log 2>&1 || exit $?
       cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $? ;;
+    benchcw0)
+      # the PPO update on k_policy_train (MAS_POL_CW=0): the counted-wait kernel's A/B
+      cd $R && MAS_POL_CW=0 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_cw0.log 2>&1 || exit $? ;;
     benchq)
       cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $?
       cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver.log 2>&1 || exit $? ;;

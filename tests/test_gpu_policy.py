@@ -231,3 +231,36 @@ def test_fused_adam_matches_torch(max_norm, grad_scale):
     opt2.load_state_dict(sd)
     fa2.bind_state()
     assert torch.equal(fa2.m, fa.m) and torch.equal(fa2.v, fa.v)
+
+
+@pytest.mark.parametrize('D,M', [(160, 8192 + 70), (468, 4096 + 2), (160, 128)])
+def test_counted_wait_train_kernel_is_bit_identical(D, M, monkeypatch):
+    """k_policy_train_cw (the PPO update's default for 32-bit store offsets)
+    only reorders the activation stores of k_policy_train: the gradients and
+    loss terms of a minibatch are bit-identical with MAS_POL_CW=0 -- full
+    blocks, a partial last block (M = 8262: 64 full 128-row blocks + 70 rows)
+    and the generic layer-1 k-loop (D = 468)."""
+    monkeypatch.setattr(ppo_mod, '_POL_LAYOUT', 'fm')
+    cfg = PPOConfig()
+    out = []
+    for cw in ('1', '0'):
+        monkeypatch.setenv('MAS_POL_CW', cw)
+        p = _policy(D, seed=D + 3)
+        fp = FusedPolicy(p, D, torch.device('cuda'))
+        fp.pack()
+        g = torch.Generator(device='cuda').manual_seed(11)
+        obs = torch.randn((M, D), device='cuda', generator=g) * 2.0
+        xb = fp.x_buffer(M)
+        acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
+        lp = torch.empty((M,), device='cuda')
+        v = torch.empty((M,), device='cuda')
+        fp.act(obs, 1, 2, acts, lp, v, xb=xb)
+        old_lp = lp + 0.3 * torch.randn((M,), device='cuda', generator=g)
+        adv = torch.randn((M,), device='cuda', generator=g)
+        ret = v + torch.randn((M,), device='cuda', generator=g)
+        terms = [float(t) for t in fp.grads(xb, acts, old_lp, adv, ret, cfg)]
+        out.append((terms, [q.grad.detach().clone() for q in p.parameters()]))
+    (t1, g1), (t0, g0) = out
+    assert t1 == t0
+    for a, b in zip(g1, g0):
+        assert torch.equal(a, b)
