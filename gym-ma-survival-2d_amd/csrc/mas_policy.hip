@@ -272,6 +272,20 @@ struct Stage1 {
     }
 };
 
+// The packed biases (b1p, b2p, b3: kBiasF floats) copied into LDS once per
+// workgroup: the per-M-tile bias reads of the layers become ds_read_b128
+// instead of global loads whose ~1-us L2 latency the layer loops waited on.
+// Ordered before every read by the first weight stage's drain + barrier.
+#ifndef MAS_POL_LDSB
+#define MAS_POL_LDSB 1
+#endif
+constexpr int kBiasF = 2 * kMT * 2 * 16 + kO;
+__device__ __forceinline__ const float* bias_lds(float* __restrict__ bl, const float* __restrict__ fb_b1)
+{
+    for (int t = (int)threadIdx.x; t < kBiasF; t += (int)blockDim.x) bl[t] = fb_b1[t];
+    return bl;
+}
+
 
 __device__ __forceinline__ void tanh_h1(const f16v (&acc)[kMT], const float* __restrict__ b1p, int h,
                                         bf8 (&h1)[kMT][2])
@@ -403,6 +417,12 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
     const Layout Lo{ks1};
     const bf8* F = reinterpret_cast<const bf8*>(packed);
     const float* FB = reinterpret_cast<const float*>(packed);
+#if MAS_POL_LDSB
+    __shared__ float bl[kBiasF];
+    const float* B1 = bias_lds(bl, FB + Lo.b1());
+#else
+    const float* B1 = FB + Lo.b1();
+#endif
     const int l = threadIdx.x & 63, h = l >> 5;
     const int64_t row0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32;
     const bool on = row0 < M;  // wave-uniform
@@ -423,9 +443,9 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x[ks];
         }
-        layer1_reg<KS>(S, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
+        layer1_reg<KS>(S, F + Lo.w1(), B1, l, on, x, h1);
     } else {
-        layer1(S, F + Lo.w1(), FB + Lo.b1(), ks1, l, on,
+        layer1(S, F + Lo.w1(), B1, ks1, l, on,
                [&](int ks) {
                    const bf8 x = x_frag_f32(obs, row, ok, D, 16 * ks + 8 * h);
                    if (xb != nullptr && ok) *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x;
@@ -433,7 +453,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
                },
                h1);
     }
-    const f16v z3 = layers23<false>(S, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);  // last barrier
+    const f16v z3 = layers23<false>(S, F + Lo.w23(), B1 + kMT * 2 * 16, l, on, h1, h2);  // last barrier
     if (!on) return;
     if (h != 0 || !ok) return;
     if (MAS_POL_EXP & 2) {
@@ -441,7 +461,7 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
         return;
     }
     float z[kO];
-    const float* b3 = FB + Lo.b3();
+    const float* b3 = B1 + 2 * kMT * 2 * 16;
 #pragma unroll
     for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
     // Gumbel-max over each head; the RNG stream of k_sample (mas_capi.hip),
@@ -871,7 +891,7 @@ __device__ __forceinline__ void stage_landed(bool issued)
 // but the last), so no store sits under a branch -- a path that skips stores
 // would leave the copies the newest operations and force vmcnt(0) waits
 template <int KS, bool OFF32, bool FULL>
-__device__ __forceinline__ void train_cw_block(const TrainArgs& A, bf8* wl, float (&st)[4])
+__device__ __forceinline__ void train_cw_block(const TrainArgs& A, bf8* wl, const float* B1, float (&st)[4])
 {
     const Layout Lo{A.ks1};
     const bf8* F = reinterpret_cast<const bf8*>(A.packed);
@@ -892,14 +912,14 @@ __device__ __forceinline__ void train_cw_block(const TrainArgs& A, bf8* wl, floa
             bf8 x[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) x[ks] = xf(ks);
-            layer1_reg<KS>(S, F + Lo.w1(), FB + Lo.b1(), l, on, x, h1);
+            layer1_reg<KS>(S, F + Lo.w1(), B1, l, on, x, h1);
         } else {
-            layer1(S, F + Lo.w1(), FB + Lo.b1(), A.ks1, l, on, xf, h1);
+            layer1(S, F + Lo.w1(), B1, A.ks1, l, on, xf, h1);
         }
         auto st2 = [&](__bf16* base, int t, const bf8 (&v)[2]) {
             if (ok) store_rows2<OFF32>(base, LD, row, t, h, v);
         };
-        const f16v z3 = layers23<true>(S, F + Lo.w23(), FB + Lo.b2(), l, on, h1, h2);
+        const f16v z3 = layers23<true>(S, F + Lo.w23(), B1 + kMT * 2 * 16, l, on, h1, h2);
         // the loss inputs of this row, loaded ahead of the activation stores
         // (a load issued after them would wait for them: vmcnt is in order);
         // the output biases through the scalar cache
@@ -1045,12 +1065,19 @@ template <int KS, bool OFF32>
 __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_policy_train_cw(TrainArgs A)
 {
     __shared__ bf8 wl[kLdsFrag];
+    const float* FB = reinterpret_cast<const float*>(A.packed);
+#if MAS_POL_LDSB
+    __shared__ float bl[kBiasF];
+    const float* B1 = bias_lds(bl, FB + Layout{A.ks1}.b1());
+#else
+    const float* B1 = FB + Layout{A.ks1}.b1();
+#endif
     const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
     float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if ((int64_t)(blockIdx.x + 1) * kTWaves * 32 <= A.M)  // block-uniform
-        train_cw_block<KS, OFF32, true>(A, wl, st);
+        train_cw_block<KS, OFF32, true>(A, wl, B1, st);
     else
-        train_cw_block<KS, OFF32, false>(A, wl, st);
+        train_cw_block<KS, OFF32, false>(A, wl, B1, st);
 
     // per-block loss partials (through the LDS stage, after its last reader)
     __syncthreads();

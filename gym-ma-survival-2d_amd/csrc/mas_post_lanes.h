@@ -29,7 +29,13 @@
 
 namespace mas {
 
-constexpr int kPostObsW = 32;  // obs column window of the LDS tile
+constexpr int kPostObsW = 32;  // obs column window of the LDS tile (MAS_POST_OBS_SEQ=0)
+// obs rows: 1 = each lane generates its own row once, in column order, and
+// stores it with 16-B (8-B, 4-B when D is not a multiple of 4 / 2) stores
+// (write_obs_row_seq); 0 = column windows of an LDS tile (write_obs_row_v)
+#ifndef MAS_POST_OBS_SEQ
+#define MAS_POST_OBS_SEQ 1
+#endif
 
 template <class C>
 struct PostLds {
@@ -54,7 +60,9 @@ struct PostLds {
             uint32_t drop[kDropW * C::AM * S];  // [field][agent][slot]
             double ang[C::AM * C::SM * S];       // DeathDrop angles, [k][slot]
         } dd;
+#if !MAS_POST_OBS_SEQ
         float tile[kWG * (kPostObsW + 1)];  // obs rows, one column window
+#endif
     } u;
 };
 
@@ -455,14 +463,153 @@ __device__ __forceinline__ void write_obs_row_v(const PostV<C>& V, const Params&
     }
 }
 
+// A lane's obs row in column order (the layout of build_layout, mas_capi.hip:
+// the observation keys sorted by name), into a sink that packs consecutive
+// columns into 16-B stores.  Same values as write_obs_row_v.
+struct SeqRow {
+    float* p;   // the row
+    int vm1;    // store width in floats - 1 (3, 1 or 0; wave-uniform)
+    int k = 0;  // next column (wave-uniform)
+    float b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, b3 = 0.0f;
+    __device__ __forceinline__ void put(float v)
+    {
+        const int s = k & vm1;
+        if (s == 0) b0 = v;
+        else if (s == 1) b1 = v;
+        else if (s == 2) b2 = v;
+        else b3 = v;
+        if (s == vm1) {
+            float* q = p + (k - s);
+            if (vm1 == 3) *reinterpret_cast<float4*>(q) = make_float4(b0, b1, b2, b3);
+            else if (vm1 == 1) *reinterpret_cast<float2*>(q) = make_float2(b0, b1);
+            else *q = b0;
+        }
+        ++k;
+    }
+};
+
+template <class C>
+__device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Params& P, uint32_t alive_m, int i,
+                                                  int lastmeta, float lhx, float lhy, SeqRow& o)
+{
+    using PV = PostV<C>;
+    const int A = P.A;
+    const bool alive = bit(alive_m, i);
+    const int pp = __popc(alive_m & ((1u << i) - 1u));  // post-despawn list position (quirk D1)
+    auto agent_row = [&](int k) {
+        const bool ak = bit(alive_m, k);
+        o.put((float)k);
+        if (P.teams) o.put((float)team_of(P, k));
+        o.put(ak ? V.ag(6, k) : 0.0f);
+#pragma unroll
+        for (int f = 0; f < 6; ++f) o.put(ak ? V.ag(f, k) : 0.0f);
+    };
+    auto seen_mask = [&](bool present, int body) -> float {
+        if (P.omniscient) return present ? 0.0f : 1.0f;
+        return (present && alive && ((V.sn(body) >> pp) & 1u)) ? 0.0f : 1.0f;
+    };
+    // agent
+    agent_row(i);
+    if (P.B > 0) {
+        // box_items, box_items_mask
+        const int ni = V.nbi();
+        for (int b = 0; b < P.B; ++b) {
+            const bool present = b < ni;
+            const float hx = V.ihx(b), hy = V.ihy(b);
+            const int rot = bi_rot(V.imeta(b));
+            const V2 ip = V.ip(b);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const V2 cv = box_corner(hx, hy, rot + v);
+                o.put(present ? cv.x : 0.0f);
+                o.put(present ? cv.y : 0.0f);
+            }
+            o.put(present ? ip.x : 0.0f);
+            o.put(present ? ip.y : 0.0f);
+        }
+        for (int b = 0; b < P.B; ++b) o.put(seen_mask(b < ni, BIdx<C>::bitem + b));
+        // box_slot, box_slot_mask
+        const bool isbox = it_kind(lastmeta) == kItemBox;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const V2 cv = box_corner(lhx, lhy, it_rot(lastmeta) + v);
+            o.put(isbox ? cv.x : 0.0f);
+            o.put(isbox ? cv.y : 0.0f);
+        }
+        o.put(isbox ? 0.0f : 1.0f);
+        // boxes, boxes_mask
+        const int nb = V.nbox();
+        for (int b = 0; b < P.B; ++b) {
+            const bool present = b < nb;
+            const int meta = V.bmeta(b);
+            const Poly4 poly = box_poly(V.bhx(b), V.bhy(b), box_rot(meta), box_copied(meta));
+            const V2 bp = V.bp(b);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                o.put(present ? poly.v[v].x : 0.0f);
+                o.put(present ? poly.v[v].y : 0.0f);
+            }
+            o.put(present ? bp.x : 0.0f);
+            o.put(present ? bp.y : 0.0f);
+            o.put(0.0f);  // box bodies always have angle 0
+        }
+        for (int b = 0; b < P.B; ++b) o.put(seen_mask(b < nb, BIdx<C>::box + b));
+    }
+    if (P.H > 0) {
+        // heal_slot, heal_slot_mask
+        const bool isheal = it_kind(lastmeta) == kItemHeal;
+        o.put(isheal ? (float)P.healing : 0.0f);
+        o.put(isheal ? 0.0f : 1.0f);
+        // heals, heals_mask
+        const int nh = V.nheal();
+        for (int h = 0; h < P.H; ++h) {
+            const bool present = h < nh;
+            const V2 hp = V.hp(h);
+            o.put(present ? hp.x : 0.0f);
+            o.put(present ? hp.y : 0.0f);
+        }
+        for (int h = 0; h < P.H; ++h) o.put(seen_mask(h < nh, BIdx<C>::heal + h));
+    }
+    // lidars: zeros here; k_lidar writes the columns afterwards
+    for (int k = 0; k < P.n_lasers; ++k) o.put(0.0f);
+    // others, others_mask (the seen list at the post-despawn list index)
+    for (int k = 0; k < A; ++k)
+        if (k != i) agent_row(k);
+    for (int k = 0; k < A; ++k) {
+        if (k == i) continue;
+        const bool ak = bit(alive_m, k);
+        o.put((alive && ak && ((V.sn(BIdx<C>::agent + k) >> pp) & 1u)) ? 0.0f : 1.0f);
+    }
+    // zone
+    const int phase = (int)V.zw(PV::kZPhase);
+    o.put(__uint_as_float(V.zw(PV::kZPx)));
+    o.put(__uint_as_float(V.zw(PV::kZPy)));
+    o.put(__uint_as_float(V.zw(PV::kZRad)));
+    float z3 = 0.0f, z4 = 0.0f, z5 = 0.0f;
+    if (phase < P.zone_phases - 1) {
+        const V2 zn = V.zc(phase + 1);
+        z3 = zn.x;
+        z4 = zn.y;
+#pragma unroll
+        for (int k = 0; k < kMaxPhases; ++k)
+            if (k == phase + 1) z5 = opq(P.zradf[k]);
+    }
+    o.put(z3);
+    o.put(z4);
+    o.put(z5);
+}
 
 // The post-physics phases of one step on agent lanes (see the file comment),
 // over env selection M (kAllEnvs / kMainEnvs on the caller's stream, the
 // slow list's kGenEnvs on the side stream).  Done envs are appended to the
 // selection's reset list (auto-reset: the k_obs reset launch over that list
 // follows, launch_post).
+// waves per SIMD the register budget targets (3: <= 168 VGPRs)
+#ifndef MAS_POST_OCC
+#define MAS_POST_OCC 3
+#endif
 template <class C, int M>
-__global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __restrict__ state, int64_t N,
+__global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint32_t* __restrict__ state, int64_t N,
                                                        float* __restrict__ obs, float* __restrict__ rew,
                                                        uint8_t* __restrict__ done, int ar)
 {
@@ -955,6 +1102,16 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
     wave_lds_sync();  // the agent table's healths and every LDS group are final
     const int D = P.D;
     const bool row_on = valid && i < A;
+#if MAS_POST_OBS_SEQ
+    if (row_on) {
+        // 16-B stores when the rows are 16-B aligned (D % 4 == 0 and a 16-B
+        // aligned buffer), else 8-B / 4-B
+        const uintptr_t ob = reinterpret_cast<uintptr_t>(obs);
+        const int vm1 = (D & 3) == 0 && (ob & 15) == 0 ? 3 : ((D & 1) == 0 && (ob & 7) == 0 ? 1 : 0);
+        SeqRow o{obs + (e * A + i) * (int64_t)D, vm1};
+        write_obs_row_seq<C>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+    }
+#else
     const int trow = j * A + i;  // tile row (the wave's rows are consecutive unless kGenEnvs)
     const int64_t r0 = M == kGenEnvs ? 0 : k0 * A;
     const int64_t rr = e * A + i;  // this lane's obs row
@@ -993,6 +1150,7 @@ __global__ __launch_bounds__(kWG, 2) void k_post_lanes(Params P, uint32_t* __res
         wave_lds_sync();  // the tile's reads are done before the next window's rows
     }
     (void)rr;
+#endif
     MAS_PROF(P, 45);
 }
 
