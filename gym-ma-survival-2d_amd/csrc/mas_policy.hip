@@ -273,11 +273,15 @@ struct Stage1 {
 };
 
 // The packed biases (b1p, b2p, b3: kBiasF floats) copied into LDS once per
-// workgroup: the per-M-tile bias reads of the layers become ds_read_b128
-// instead of global loads whose ~1-us L2 latency the layer loops waited on.
-// Ordered before every read by the first weight stage's drain + barrier.
+// workgroup (MAS_POL_LDSB=1): the per-M-tile bias reads of the layers become
+// ds_read_b128 instead of global loads.  Measured slower (r04g: train 3.53 vs
+// 3.21 ms, act 121 vs 114 us): the MFMA loops read a 1-KiB weight fragment
+// from LDS per 32-cycle MFMA on every SIMD, the CU's whole 128 B/clk, so LDS
+// bias reads steal weight bandwidth, while the global bias loads the compiler
+// issues early are hidden.  Off by default.  Ordered before every read by the
+// first weight stage's drain + barrier.
 #ifndef MAS_POL_LDSB
-#define MAS_POL_LDSB 1
+#define MAS_POL_LDSB 0
 #endif
 constexpr int kBiasF = 2 * kMT * 2 * 16 + kO;
 __device__ __forceinline__ const float* bias_lds(float* __restrict__ bl, const float* __restrict__ fb_b1)
@@ -1099,6 +1103,332 @@ __global__ __launch_bounds__(64 * kTWaves, MAS_POL_OCC * 4 / kTWaves) void k_pol
 }
 
 // ---------------------------------------------------------------------------
+// k_policy_train_db: the PPO update's train kernel as one persistent
+// 8-wave workgroup per CU with DOUBLE-BUFFERED weight stages (2 x 72 KiB of
+// the CU's 160 KiB LDS).  k_policy_train runs two 4-wave workgroups per CU on
+// one 72-KiB stage each: every stage boundary (7 per 128-row block) drains
+// the stage's LDS-DMA copies -- and, vmcnt being in issue order, every
+// activation store before them -- with the waves parked at the barrier, and
+// hopes the other workgroup computes meanwhile.  Here a boundary waits only
+// for copies issued a whole phase earlier: phase p starts by issuing the
+// copies of stage p + 1 into the other buffer (all waves are past phase p - 1,
+// the buffer's last reader), then the stores of activations finished earlier,
+// then computes from buffer p; the landing of stage p + 1 waits with
+// vmcnt(n), n the wave's vector memory operations issued after those copies
+// (counted per phase below, capped at 63: the counter saturates, so 63
+// outstanding implies every older operation done).  8 waves share each
+// stage: 256 rows per weight pass instead of 128.  Full 256-row blocks only
+// (straight-line stores, exact counts); the partial last block goes to
+// k_policy_train (policy_train).  Same operations in the same order per row:
+// bit-identical to k_policy_train (test_counted_wait_train_kernel_is_bit_identical).
+// ---------------------------------------------------------------------------
+#ifndef MAS_POL_DB_SB
+#define MAS_POL_DB_SB 1
+#endif
+constexpr int kDW = 8;                  // waves per workgroup
+constexpr int kDRows = 32 * kDW;        // rows per block
+constexpr int kDCopy = 64 * kDW;        // fragments one copy round moves (one per thread)
+static_assert(kLdsFrag % kDCopy == 0 && (kBk0 * 64) % kDCopy == 0 && (kBk1 * 64) % kDCopy == 0, "copy rounds");
+
+// LDS-DMA copy of n fragments (n a multiple of kDCopy, wave-uniform), no
+// wait.  Written as inline asm (global_load_lds_dwordx4 with the wave's
+// global base in SGPRs, the lane's 16-B offset in one VGPR, the LDS base in
+// m0): with the builtin, the compiler's wait-count pass cannot tell the next
+// stage's buffer from the current one and waits for these copies (vmcnt(0),
+// every store before them included) at the phase's first LDS read -- the
+// serialisation this kernel removes.  Invisible to that pass, the copies are
+// ordered only by land_db's explicit counts; the pass's own waits for other
+// loads can only over-wait (it does not count these).  m0 is set before every
+// copy: no other m0 user runs in this kernel.
+__device__ __forceinline__ void copy_db(bf8* __restrict__ buf, const bf8* __restrict__ src, int n)
+{
+    const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+    const uint32_t loff = (threadIdx.x & 63) * 16u;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(buf) + w0 * 16u;  // LDS byte offset
+    const uint8_t* g0 = reinterpret_cast<const uint8_t*>(src) + w0 * 16u;
+    for (int k = 0; k < n; k += kDCopy) {
+        const uint32_t m0v = lds0 + (uint32_t)k * 16u;
+        const uint8_t* gk = g0 + (int64_t)k * 16;
+        asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0v), "v"(loff), "s"(gk) : "memory");
+    }
+}
+// the stage copied one phase ago has landed in every wave: NST = this wave's
+// vector memory operations issued after those copies (a lower bound)
+template <int NST>
+__device__ __forceinline__ void land_db()
+{
+    constexpr int n = NST > 63 ? 63 : NST;
+    __builtin_amdgcn_s_waitcnt((n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+    lds_barrier();
+}
+
+template <int KS, bool OFF32>
+__global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, int64_t nblk)
+{
+    static_assert(KS > 0, "compile-time layer-1 depth");
+    constexpr int NCH = (KS + kKc - 1) / kKc;  // layer-1 stages
+    __shared__ bf8 wl[2 * kLdsFrag];
+    __shared__ float bl[kBiasF];
+    __shared__ float red[kDW * 4];
+    const Layout Lo{A.ks1};
+    const bf8* F = reinterpret_cast<const bf8*>(A.packed);
+    const float* FB = reinterpret_cast<const float*>(A.packed);
+    bias_lds(bl, FB + Lo.b1());
+    const float* b1p = bl;
+    const float* b2p = bl + kMT * 2 * 16;
+    const float* b3 = bl + 2 * kMT * 2 * 16;
+    const int l0 = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t LD = A.ld;
+    float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int sc = 0;  // stages so far: the current one is in buffer sc & 1
+    auto buf = [&](int k) { return wl + (k & 1) * kLdsFrag; };
+    // (each tile's 8 stores fenced off from the scheduler: a burst of
+    // interleaved tiles' pair shuffles would spill)
+    auto st2 = [&](__bf16* base, int64_t row, int t, int h, const bf8 (&v)[2]) {
+        // (row re-materialised per tile: CSE'd across the buffers, the 64
+        // per-word store offsets stayed live from phase C to G and spilled)
+        asm volatile("" : "+v"(row));
+        store_rows2<OFF32>(base, LD, row, t, h, v);
+#if MAS_POL_DB_SB
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+    };
+    const int64_t b0 = blockIdx.x;
+    if (b0 < nblk) copy_db(buf(0), F + Lo.w1(), (KS < kKc ? KS : kKc) * kMT * 64);  // prologue
+    for (int64_t blk = b0; blk < nblk; blk += gridDim.x) {
+        // the lane index made opaque per block: keeps the compiler from
+        // hoisting the blocks' LDS and store addresses out of the loop (held
+        // live across it they spilled)
+        int l = l0;
+        asm volatile("" : "+v"(l));
+        const int h = l >> 5;
+        const int64_t row = blk * kDRows + wv * 32 + (l & 31);
+        bf8 h1[kMT][2], h2[kMT][2];
+        // the loss inputs of the row (read in phase E)
+        uint32_t aw0 = 0, aw1 = 0;  // the row's 6 action bytes: 0..3, 4..5
+        float adv = 0.0f, old_lp = 0.0f, ret = 0.0f;
+        // ---- layer 1: NCH stages of up to kKc k-steps
+        {
+            f16v acc[kMT];
+#pragma unroll
+            for (int mt = 0; mt < kMT; ++mt) acc[mt] = f16v{};
+            bf8 x[KS];
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                if (c == 0) {
+                    if (blk == b0) land_db<0>();   // the prologue's copies
+                    else land_db<32>();            // phase G: 32 dA1 stores after them
+                } else {
+                    if (c == 1) land_db<KS>();  // chunk 0: the x loads after them
+                    else land_db<0>();
+                }
+                const bf8* w = buf(sc);
+                if (c + 1 < NCH) {
+                    const int k1 = (c + 1) * kKc, kn = KS - k1 < kKc ? KS - k1 : kKc;
+                    copy_db(buf(sc + 1), F + Lo.w1() + k1 * kMT * 64, kn * kMT * 64);
+                } else {
+                    copy_db(buf(sc + 1), F + Lo.w23(), kHalf * 64);
+                }
+                if (c == 0) {
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks)
+                        x[ks] = *reinterpret_cast<const bf8*>(A.xb + row * A.xb_stride + 16 * ks + 8 * h);
+                }
+                const int kn = KS - c * kKc < kKc ? KS - c * kKc : kKc;
+#pragma unroll
+                for (int q = 0; q < kn; ++q) {
+                    const bf8* wk = w + q * kMT * 64 + l;
+#pragma unroll
+                    for (int mt = 0; mt < kMT; ++mt) acc[mt] = mfma(wk[mt * 64], x[c * kKc + q], acc[mt]);
+                }
+                ++sc;
+            }
+            tanh_h1(acc, b1p, h, h1);
+        }
+        // ---- layers 2 + 3: two half stages (C, D)
+        f16v z3 = f16v{};
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            if (hf == 0) land_db<NCH == 1 ? KS : 0>();
+            else land_db<64>();  // phase C: 64 h1 stores after them
+            const bf8* wl2 = buf(sc);
+            if (hf == 0) {
+                copy_db(buf(sc + 1), F + Lo.w23() + kHalf * 64, kHalf * 64);
+#pragma unroll
+                for (int mt = 0; mt < kMT; ++mt) st2(A.h1, row, mt, h, h1[mt]);  // 64 stores
+            } else {
+                copy_db(buf(sc + 1), F + Lo.wbk(), kBk0 * 64);
+                // the loss inputs of the row (read in phase E)
+                const uint16_t* ap = reinterpret_cast<const uint16_t*>(A.act + row * 6);
+                aw0 = (uint32_t)ap[0] | ((uint32_t)ap[1] << 16);
+                aw1 = ap[2];
+                adv = A.adv[row];
+                old_lp = A.old_logp[row];
+                ret = A.ret[row];
+#pragma unroll
+                for (int mt = 0; mt < kMT / 2; ++mt) st2(A.h2, row, mt, h, h2[mt]);  // 32 stores
+            }
+#pragma unroll
+            for (int q = 0; q < kMT / 2; ++q) {
+                const int mo = kMT / 2 * hf + q;
+                f16v a = f16v{};
+                const bf8* w = wl2 + q * 16 * 64 + l;
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) a = mfma(w[kk * 64], h1[kk >> 1][kk & 1], a);
+                float b[16];
+                load16(b2p + (mo * 2 + h) * 16, b);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) h2[mo][i >> 3][i & 7] = (__bf16)tanh_pre(a[i], b[i]);
+                const bf8* w3 = wl2 + (kMT / 2 * 16 + 2 * q) * 64 + l;
+                z3 = mfma(w3[0], h2[mo][0], z3);
+                z3 = mfma(w3[64], h2[mo][1], z3);
+            }
+            ++sc;
+        }
+        // the loss inputs consumed on every lane here, at the end of phase D:
+        // their wait then sits in straight-line code (read only inside the
+        // lane-half branch, they would stay pending in the compiler's
+        // wait-count state on the branch-skipping path, around the block loop,
+        // and force a full vmcnt(0) at the next reuse of their registers)
+        // (a memory clobber anchors it after the phase's LDS reads and stores)
+        // (in-out operands: nothing derived from them is computed before)
+        asm volatile("" : "+v"(aw0), "+v"(aw1), "+v"(adv), "+v"(old_lp), "+v"(ret)::"memory");
+        // ---- E: W3^T; the loss gradient, dA2
+        land_db<38>();  // phase D: 6 loss-input loads + 32 h2 stores after them
+        const bf8* wb = buf(sc);
+        copy_db(buf(sc + 1), F + Lo.wbk() + kBk0 * 64, kBk1 * 64);
+#pragma unroll
+        for (int mt = kMT / 2; mt < kMT; ++mt) st2(A.h2, row, mt, h, h2[mt]);  // 32 stores
+        float dz[kO];
+#pragma unroll
+        for (int o = 0; o < kO; ++o) dz[o] = 0.0f;
+        if (h == 0) {
+            float z[kO];
+#pragma unroll
+            for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
+            int a[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) a[k] = (int)(int8_t)(((k < 4 ? aw0 : aw1) >> (8 * (k & 3))) & 0xffu);
+            // (log-softmax and probabilities recomputed in the gradient loop
+            // from the heads' lse: the same values, 30 fewer live registers)
+            float lse[6], hent[6];
+            float lp = 0.0f, ent = 0.0f;
+#pragma unroll
+            for (int hd = 0; hd < 6; ++hd) {
+                const int n = kHeadN[hd], off = kHeadOff[hd];
+                float mx = z[off];
+#pragma unroll
+                for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
+                float se = 0.0f;
+#pragma unroll
+                for (int k = 0; k < n; ++k) se += exp_fast(z[off + k] - mx);
+                lse[hd] = mx + log_fast(se);
+                float e = 0.0f;
+                const int ak = a[hd];
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    const float lsm = z[off + k] - lse[hd];
+                    const float p = exp_fast(lsm);
+                    e -= p * lsm;
+                    if (k == ak) lp += lsm;
+                }
+                hent[hd] = e;
+                ent += e;
+            }
+            const float ratio = exp_fast(lp - old_lp);
+            const float s1 = ratio * adv;
+            const float rc = fminf(fmaxf(ratio, 1.0f - A.clip), 1.0f + A.clip);
+            const float s2 = rc * adv;
+            const float glp = s1 <= s2 ? -s1 : 0.0f;
+            const float sc_ = A.scale;
+#pragma unroll
+            for (int hd = 0; hd < 6; ++hd) {
+                const int n = kHeadN[hd], off = kHeadOff[hd];
+                const int ak = a[hd];
+#pragma unroll
+                for (int k = 0; k < n; ++k) {
+                    const float oh = k == ak ? 1.0f : 0.0f;
+                    const float lsm = z[off + k] - lse[hd];
+                    const float p = exp_fast(lsm);
+                    dz[off + k] = sc_ * (glp * (oh - p) + A.ent_coef * p * (lsm + hent[hd]));
+                }
+            }
+            const float dv = z[kO - 1] - ret;
+            dz[kO - 1] = sc_ * A.vf_coef * 2.0f * dv;
+            st[0] += -fminf(s1, s2);
+            st[1] += dv * dv;
+            st[2] += ent;
+            st[3] += fabsf(ratio - 1.0f) > A.clip ? 1.0f : 0.0f;
+#pragma unroll
+            for (int o = 0; o < kO; ++o) A.dz[(int64_t)o * LD + row] = (__bf16)dz[o];
+        }
+        bf8 dzf[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dzf[i >> 3][i & 7] = (__bf16)dz[i];
+        bf8 da2[kMT][2];
+#pragma unroll
+        for (int mo = 0; mo < kMT; ++mo) {
+            f16v g = f16v{};
+            g = mfma(wb[(mo * 2) * 64 + l], dzf[0], g);
+            g = mfma(wb[(mo * 2 + 1) * 64 + l], dzf[1], g);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float hv = (float)h2[mo][i >> 3][i & 7];
+                da2[mo][i >> 3][i & 7] = (__bf16)(g[i] * dtanh(hv));
+            }
+            st2(A.da2, row, mo, h, da2[mo]);  // 64 stores
+        }
+        ++sc;
+        // ---- F, G: W2^T halves; dA1
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            if (hf == 0) land_db<96>();  // phase E: 32 h2 + 64 dA2 stores (+ 16 dz) after them
+            else land_db<32>();          // phase F: 32 dA1 stores
+            const bf8* W2T = buf(sc);
+            if (hf == 0) copy_db(buf(sc + 1), F + Lo.wbk() + (kBk0 + kBk1) * 64, kBk1 * 64);
+            else if (blk + gridDim.x < nblk) copy_db(buf(sc + 1), F + Lo.w1(), (KS < kKc ? KS : kKc) * kMT * 64);
+#pragma unroll
+            for (int q = 0; q < kMT / 2; ++q) {
+                const int mt = kMT / 2 * hf + q;
+                f16v g = f16v{};
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) g = mfma(W2T[(q * 16 + kk) * 64 + l], da2[kk >> 1][kk & 1], g);
+                bf8 d1[2];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float hv = (float)h1[mt][i >> 3][i & 7];
+                    d1[i >> 3][i & 7] = (__bf16)(g[i] * dtanh(hv));
+                }
+                st2(A.da1, row, mt, h, d1);  // 8 stores
+            }
+            ++sc;
+        }
+    }
+    const int l = l0;
+    // per-workgroup loss partials: row 2 b0 (this workgroup's first block), zeros in the
+    // other rows of its blocks (two 128-row partial rows per 256-row block)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float v = st[k];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (l == 0) red[wv * 4 + k] = v;
+    }
+    __syncthreads();
+    for (int64_t blk = b0; blk < nblk; blk += gridDim.x) {
+        if (threadIdx.x < 8) {
+            const int k = (int)threadIdx.x & 3;
+            float v = 0.0f;
+            if (blk == b0 && threadIdx.x < 4) {
+#pragma unroll
+                for (int w = 0; w < kDW; ++w) v += red[w * 4 + k];
+            }
+            A.partials[(2 * blk + (threadIdx.x >> 2)) * 4 + k] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradients of one minibatch, dW = A B^T and db = row sums of A, over
 // the minibatch rows K: A [F][K] (dA2 or dz) and B [G][K] (h1 or h2) are the
 // feature-major bf16 activations mas_policy_train writes (K contiguous, row
@@ -1513,6 +1843,42 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
     // offsets that only buffers over 4 GB take, on any size
     const char* f64 = getenv("MAS_POL_FORCE_OFF64");
     const bool o32 = ld <= pol::kOff32Ld && !(f64 && f64[0] == '1');
+    // the persistent double-buffered kernel for the full 256-row blocks of the
+    // PPO update's store mode (feature-major, two rows per lane, 32-bit
+    // offsets, compile-time layer-1 depth), k_policy_train for the rest;
+    // MAS_POL_DB=0: k_policy_train_cw / k_policy_train only
+    const char* db = getenv("MAS_POL_DB");
+    const int64_t nfull = M / pol::kDRows;
+    if (!rm && o32 && (A.ks1 == 10 || A.ks1 == 9) && ((M | ld) & 1) == 0 && nfull > 0 && !(db && db[0] == '0')) {
+        static int ncu = 0;
+        if (ncu == 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                ncu = 256;
+        }
+        const int64_t grid = nfull < ncu ? nfull : ncu;
+        auto kd = A.ks1 == 10 ? pol::k_policy_train_db<10, true> : pol::k_policy_train_db<9, true>;
+        hipLaunchKernelGGL(kd, dim3((unsigned)grid), dim3(64 * pol::kDW), 0, s, A, nfull);
+        const int64_t r0 = nfull * pol::kDRows;
+        if (r0 < M) {  // the partial last block: k_policy_train on offset buffers
+            pol::TrainArgs T = A;
+            T.M = M - r0;
+            T.xb = A.xb + r0 * A.xb_stride;
+            T.act = A.act + r0 * 6;
+            T.old_logp = A.old_logp + r0;
+            T.adv = A.adv + r0;
+            T.ret = A.ret + r0;
+            T.h1 = A.h1 + r0;
+            T.h2 = A.h2 + r0;
+            T.da1 = A.da1 + r0;
+            T.da2 = A.da2 + r0;
+            T.dz = A.dz + r0;
+            T.partials = A.partials + 2 * nfull * 4;
+            auto kt = A.ks1 == 10 ? pol::k_policy_train<10, true, false> : pol::k_policy_train<9, true, false>;
+            hipLaunchKernelGGL(kt, dim3((unsigned)policy_blocks(T.M)), dim3(64 * pol::kTWaves), 0, s, T);
+        }
+        return hipGetLastError();
+    }
     // the counted-wait kernel for the PPO update's store mode (feature-major,
     // two rows per lane: M and ld even) with 32-bit store offsets; its 64-bit
     // offset and 9-k-step layer-1 builds spill (compiler resource report), so

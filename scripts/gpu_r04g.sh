@@ -11,8 +11,10 @@ for v in "" _tile _seq2; do
   timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline --lib $L/libmas$v.so > $O/bench_ffa$v.log 2>&1 || exit $?
   timeout -k 10 200 python bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline --lib $L/libmas$v.so > $O/bench_1v1$v.log 2>&1 || exit $?
 done
-for cw in 1 0; do
-  MAS_POL_CW=$cw timeout -k 10 300 python -u scripts/policy_bench.py $L/libmas.so $L/libmas_nolds.so $L/libmas_nodefer.so > $O/polbench_cw$cw.log 2>&1 || exit $?
+for v in "MAS_POL_DB=1 MAS_POL_CW=1" "MAS_POL_DB=0 MAS_POL_CW=1" "MAS_POL_DB=0 MAS_POL_CW=0"; do
+  env $v timeout -k 10 300 python -u scripts/policy_bench.py $L/libmas.so $L/libmas_nolds.so >> $O/polbench.log 2>&1 || exit $?
+  echo "^ $v" >> $O/polbench.log
 done
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver.log 2>&1 || exit $?
+MAS_POL_DB=0 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_db0.log 2>&1 || exit $?
 echo ok
