@@ -274,11 +274,14 @@ struct Stage1 {
 
 // The packed biases (b1p, b2p, b3: kBiasF floats) copied into LDS once per
 // workgroup (MAS_POL_LDSB=1): the per-M-tile bias reads of the layers become
-// ds_read_b128 instead of global loads.  Measured slower (r04g: train 3.53 vs
-// 3.21 ms, act 121 vs 114 us): the MFMA loops read a 1-KiB weight fragment
-// from LDS per 32-cycle MFMA on every SIMD, the CU's whole 128 B/clk, so LDS
-// bias reads steal weight bandwidth, while the global bias loads the compiler
-// issues early are hidden.  Off by default.  Ordered before every read by the
+// ds_read_b128 instead of global loads.  No gain measured (r04g: the A/B
+// was within policy_bench's run-order bias -- the same train kernel timed
+// 3.88 vs 3.52 ms as first vs second library of one process): the MFMA
+// loops read a 1-KiB weight fragment from LDS per 32-cycle MFMA on every
+// SIMD, the CU's whole 128 B/clk, so LDS bias reads compete with the weight
+// reads, while the global bias loads the compiler issues early are mostly
+// hidden.  Off by default (k_policy_train_db always stages them: its
+// double-buffered layout has the room).  Ordered before every read by the
 // first weight stage's drain + barrier.
 #ifndef MAS_POL_LDSB
 #define MAS_POL_LDSB 0
