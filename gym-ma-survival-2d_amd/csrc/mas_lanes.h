@@ -104,26 +104,83 @@ __device__ __forceinline__ T env_bcast(T v, int src)
 
 // the cooperative load / store of one state group's words for the wave's
 // env slots: lane l moves word l / S of slot l % S, kWG / S words per
-// instruction (each word's S envs are one contiguous row segment)
-template <int S>
-__device__ __forceinline__ void group_load(uint32_t* __restrict__ dst, const uint32_t* __restrict__ state, int64_t N,
-                                           int64_t e0, int w0, int nw)
-{
-    const int lane = (int)threadIdx.x;
-    for (int idx = lane; idx < nw * S; idx += kWG) {
-        const int w = idx / S, j = idx - w * S;
-        const int64_t e = e0 + j < N ? e0 + j : N - 1;
-        dst[idx] = state[state_index(w0 + w, e, N)];
+// instruction (each word's S envs are one contiguous row segment).  Unrolled
+// over the group's kWG-word rounds with every load issued before the first
+// LDS write: the rolled loop waited out one load latency per round (round
+// r04h: 7 rounds for the 2v2 box group, four groups back to back).
+// (split in two so that a kernel issues every group's loads -- and its
+// per-lane state loads -- before the first LDS write: the compiler keeps
+// global loads below earlier LDS stores it cannot prove disjoint)
+template <int S, int NW>
+struct GroupRows {
+    static constexpr int T = (NW * S + kWG - 1) / kWG;
+    uint32_t v[T];
+    __device__ __forceinline__ void load(const uint32_t* __restrict__ state, int64_t N, int64_t e0, int w0)
+    {
+        const int lane = (int)threadIdx.x;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int i0 = lane + t * kWG;
+            const int idx = i0 < NW * S ? i0 : NW * S - 1;  // (clamped: every load unconditional)
+            const int w = idx / S, j = idx - w * S;
+            const int64_t e = e0 + j < N ? e0 + j : N - 1;
+            v[t] = state[state_index(w0 + w, e, N)];
+        }
     }
-}
-template <int S>
+    __device__ __forceinline__ void write(uint32_t* __restrict__ dst) const
+    {
+        const int lane = (int)threadIdx.x;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int idx = lane + t * kWG;
+            if (idx < NW * S) dst[idx] = v[t];
+        }
+    }
+    // load + write in chunks of 8 rounds (the big classes' groups: fewer live
+    // registers, still 8 loads in flight)
+    __device__ __forceinline__ static void copy(uint32_t* __restrict__ dst, const uint32_t* __restrict__ state,
+                                                int64_t N, int64_t e0, int w0)
+    {
+        const int lane = (int)threadIdx.x;
+#pragma unroll
+        for (int c0 = 0; c0 < T; c0 += 8) {
+            uint32_t u[8];
+#pragma unroll
+            for (int t = c0; t < c0 + 8 && t < T; ++t) {
+                const int i0 = lane + t * kWG;
+                const int idx = i0 < NW * S ? i0 : NW * S - 1;
+                const int w = idx / S, j = idx - w * S;
+                const int64_t e = e0 + j < N ? e0 + j : N - 1;
+                u[t - c0] = state[state_index(w0 + w, e, N)];
+            }
+#pragma unroll
+            for (int t = c0; t < c0 + 8 && t < T; ++t) {
+                const int idx = lane + t * kWG;
+                if (idx < NW * S) dst[idx] = u[t - c0];
+            }
+        }
+    }
+};
+template <int S, int NW>
 __device__ __forceinline__ void group_store(const uint32_t* __restrict__ src, uint32_t* __restrict__ state, int64_t N,
-                                            int64_t e0, int w0, int nw, uint32_t slots)
+                                            int64_t e0, int w0, uint32_t slots)
 {
+    constexpr int T = (NW * S + kWG - 1) / kWG;
     const int lane = (int)threadIdx.x;
-    for (int idx = lane; idx < nw * S; idx += kWG) {
-        const int w = idx / S, j = idx - w * S;
-        if (((slots >> j) & 1u) && e0 + j < N) state[state_index(w0 + w, e0 + j, N)] = src[idx];
+#pragma unroll
+    for (int c0 = 0; c0 < T; c0 += 8) {  // chunks of 8 rounds: LDS reads, then stores
+        uint32_t v[8];
+#pragma unroll
+        for (int t = c0; t < c0 + 8 && t < T; ++t) {
+            const int i0 = lane + t * kWG;
+            v[t - c0] = src[i0 < NW * S ? i0 : NW * S - 1];
+        }
+#pragma unroll
+        for (int t = c0; t < c0 + 8 && t < T; ++t) {
+            const int idx = lane + t * kWG;
+            const int w = idx / S, j = idx - w * S;
+            if (idx < NW * S && ((slots >> j) & 1u) && e0 + j < N) state[state_index(w0 + w, e0 + j, N)] = v[t - c0];
+        }
     }
 }
 
@@ -369,10 +426,24 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
     }
     const EnvV<C> V{&lds, j};
     // ---- state: the env-shared groups into LDS, this lane's agent into registers
-    group_load<S>(lds.box, state, N, e0, LY::box, LY::kBoxW);
-    group_load<S>(lds.item, state, N, e0, LY::item, LY::kItemW);
-    group_load<S>(lds.pend, state, N, e0, LY::pend, LY::kItemW);
-    group_load<S>(lds.heal, state, N, e0, LY::heal, LY::kHealW);
+    GroupRows<S, LY::kBoxW> rbox;
+    GroupRows<S, LY::kItemW> ritem, rpend;
+    GroupRows<S, LY::kHealW> rheal;
+    // all four groups' loads in flight at once when their registers fit
+    // (2v2: 22 words per lane); the big classes (ffa: 76) write each group
+    // as soon as its loads are issued
+    constexpr bool kBatch = decltype(rbox)::T + 2 * decltype(ritem)::T + decltype(rheal)::T <= 24;
+    if (kBatch) {
+        rbox.load(state, N, e0, LY::box);
+        ritem.load(state, N, e0, LY::item);
+        rpend.load(state, N, e0, LY::pend);
+        rheal.load(state, N, e0, LY::heal);
+    } else {
+        decltype(rbox)::copy(lds.box, state, N, e0, LY::box);
+        decltype(ritem)::copy(lds.item, state, N, e0, LY::item);
+        decltype(rpend)::copy(lds.pend, state, N, e0, LY::pend);
+        decltype(rheal)::copy(lds.heal, state, N, e0, LY::heal);
+    }
     AgentL<C> g;
     {
         float d[7];
@@ -407,10 +478,14 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
     int ac[6];
     bool bad = false;
     {
-        const int8_t* ar = actions + (ev * A + (i < A ? i : A - 1)) * 6;
+        // (three 2-B loads, issued on every lane: a lane past A reads agent
+        // A - 1's row and drops it)
+        const uint16_t* ar = reinterpret_cast<const uint16_t*>(actions + (ev * A + (i < A ? i : A - 1)) * 6);
+        const uint32_t a01 = ar[0], a23 = ar[1], a45 = ar[2];
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            const int x = i < A ? (int)ar[k] : 0;
+            const uint32_t word = k < 2 ? a01 : (k < 4 ? a23 : a45);
+            const int x = i < A ? (int)(int8_t)((word >> (8 * (k & 1))) & 0xffu) : 0;
             const int hi = k < 3 ? 2 : 1;
             bad = bad || x < 0 || x > hi;
             ac[k] = x < 0 ? 0 : (x > hi ? hi : x);
@@ -422,6 +497,12 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
         const bool env_bad = env_ballot<C>(bad) != 0u && valid && i == 0;
         const uint64_t m = __ballot(env_bad);
         if (m && lane == __ffsll((unsigned long long)m) - 1) atomicAdd(P.bad_actions, __popcll(m));
+    }
+    if (kBatch) {
+        rbox.write(lds.box);
+        ritem.write(lds.item);
+        rpend.write(lds.pend);
+        rheal.write(lds.heal);
     }
     lds.ax[i * S + j] = g.c.x;
     lds.ay[i * S + j] = g.c.y;
@@ -642,9 +723,9 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
             si |= (uint32_t)((mi >> (q * AM)) & 1ull) << q;
             sp |= (uint32_t)((mp >> (q * AM)) & 1ull) << q;
         }
-        if (sb) group_store<S>(lds.box, state, N, e0, LY::box, LY::kBoxW, sb);
-        if (si) group_store<S>(lds.item, state, N, e0, LY::item, LY::kItemW, si);
-        if (sp) group_store<S>(lds.pend, state, N, e0, LY::pend, LY::kItemW, sp);
+        if (sb) group_store<S, LY::kBoxW>(lds.box, state, N, e0, LY::box, sb);
+        if (si) group_store<S, LY::kItemW>(lds.item, state, N, e0, LY::item, si);
+        if (sp) group_store<S, LY::kItemW>(lds.pend, state, N, e0, LY::pend, sp);
     }
     MAS_PROF(P, 23);
     // ---------------- speculative contact-free physics (fast_phys) ----------------

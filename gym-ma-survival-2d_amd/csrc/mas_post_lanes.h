@@ -99,23 +99,75 @@ struct PostV {
 };
 
 // env-slot table versions of the cooperative row loads / stores (the slots'
-// envs need not be consecutive: the slow list)
-template <int S>
-__device__ __forceinline__ void slot_load(uint32_t* __restrict__ dst, const uint32_t* __restrict__ state, int64_t N,
-                                          const int64_t* eidx, int w0, int nw)
-{
-    for (int idx = (int)threadIdx.x; idx < nw * S; idx += kWG) {
-        const int w = idx / S, j = idx - w * S;
-        dst[idx] = state[state_index(w0 + w, eidx[j], N)];
+// envs need not be consecutive: the slow list); unrolled like group_load
+template <int S, int NW>
+struct SlotRows {
+    static constexpr int T = (NW * S + kWG - 1) / kWG;
+    uint32_t v[T];
+    __device__ __forceinline__ void load(const uint32_t* __restrict__ state, int64_t N, const int64_t* eidx, int w0)
+    {
+        const int lane = (int)threadIdx.x;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int i0 = lane + t * kWG;
+            const int idx = i0 < NW * S ? i0 : NW * S - 1;
+            const int w = idx / S, j = idx - w * S;
+            v[t] = state[state_index(w0 + w, eidx[j], N)];
+        }
     }
-}
-template <int S>
+    __device__ __forceinline__ void write(uint32_t* __restrict__ dst) const
+    {
+        const int lane = (int)threadIdx.x;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int idx = lane + t * kWG;
+            if (idx < NW * S) dst[idx] = v[t];
+        }
+    }
+    // load + write in chunks of 8 rounds (GroupRows::copy)
+    __device__ __forceinline__ static void copy(uint32_t* __restrict__ dst, const uint32_t* __restrict__ state,
+                                                int64_t N, const int64_t* eidx, int w0)
+    {
+        const int lane = (int)threadIdx.x;
+#pragma unroll
+        for (int c0 = 0; c0 < T; c0 += 8) {
+            uint32_t u[8];
+#pragma unroll
+            for (int t = c0; t < c0 + 8 && t < T; ++t) {
+                const int i0 = lane + t * kWG;
+                const int idx = i0 < NW * S ? i0 : NW * S - 1;
+                const int w = idx / S, j = idx - w * S;
+                u[t - c0] = state[state_index(w0 + w, eidx[j], N)];
+            }
+#pragma unroll
+            for (int t = c0; t < c0 + 8 && t < T; ++t) {
+                const int idx = lane + t * kWG;
+                if (idx < NW * S) dst[idx] = u[t - c0];
+            }
+        }
+    }
+};
+template <int S, int NW>
 __device__ __forceinline__ void slot_store(const uint32_t* __restrict__ src, uint32_t* __restrict__ state, int64_t N,
-                                           const int64_t* eidx, int w0, int nw, uint32_t slots)
+                                           const int64_t* eidx, int w0, uint32_t slots)
 {
-    for (int idx = (int)threadIdx.x; idx < nw * S; idx += kWG) {
-        const int w = idx / S, j = idx - w * S;
-        if ((slots >> j) & 1u) state[state_index(w0 + w, eidx[j], N)] = src[idx];
+    constexpr int T = (NW * S + kWG - 1) / kWG;
+    const int lane = (int)threadIdx.x;
+    const int64_t ex = eidx[lane % S];  // (a round's lanes hold slots lane % S: kWG is a multiple of S)
+#pragma unroll
+    for (int c0 = 0; c0 < T; c0 += 8) {  // chunks of 8 rounds: LDS reads, then stores
+        uint32_t v[8];
+#pragma unroll
+        for (int t = c0; t < c0 + 8 && t < T; ++t) {
+            const int i0 = lane + t * kWG;
+            v[t - c0] = src[i0 < NW * S ? i0 : NW * S - 1];
+        }
+#pragma unroll
+        for (int t = c0; t < c0 + 8 && t < T; ++t) {
+            const int idx = lane + t * kWG;
+            const int w = idx / S, j = idx - w * S;
+            if (idx < NW * S && ((slots >> j) & 1u)) state[state_index(w0 + w, ex, N)] = v[t - c0];
+        }
     }
 }
 
@@ -636,10 +688,25 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
     wave_lds_sync();
     const PV V{&lds, j};
     // ---- state: the env-shared groups into LDS, this lane's agent into registers
-    slot_load<S>(lds.box, state, N, lds.eidx, LY::box, LY::kBoxW);
-    slot_load<S>(lds.item, state, N, lds.eidx, LY::item, LY::kItemW);
-    slot_load<S>(lds.heal, state, N, lds.eidx, LY::heal, LY::kHealW);
-    slot_load<S>(lds.zone, state, N, lds.eidx, LY::zone, LY::kZoneW);
+    // every group's loads and this lane's agent loads first, then the LDS
+    // writes (SlotRows)
+    SlotRows<S, LY::kBoxW> rbox;
+    SlotRows<S, LY::kItemW> ritem;
+    SlotRows<S, LY::kHealW> rheal;
+    SlotRows<S, LY::kZoneW> rzone;
+    // (all in flight at once only when the registers fit the 3-wave budget)
+    constexpr bool kBatch = decltype(rbox)::T + decltype(ritem)::T + decltype(rheal)::T + decltype(rzone)::T <= 16;
+    if (kBatch) {
+        rbox.load(state, N, lds.eidx, LY::box);
+        ritem.load(state, N, lds.eidx, LY::item);
+        rheal.load(state, N, lds.eidx, LY::heal);
+        rzone.load(state, N, lds.eidx, LY::zone);
+    } else {
+        decltype(rbox)::copy(lds.box, state, N, lds.eidx, LY::box);
+        decltype(ritem)::copy(lds.item, state, N, lds.eidx, LY::item);
+        decltype(rheal)::copy(lds.heal, state, N, lds.eidx, LY::heal);
+        decltype(rzone)::copy(lds.zone, state, N, lds.eidx, LY::zone);
+    }
     AgentL<C> g;
     {
         float d[6];
@@ -665,6 +732,12 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
     uint32_t alive_m = state[state_index(LY::alive, e, N)];
     uint32_t awake_m = state[state_index(LY::awake, e, N)];
     bool alive = bit(alive_m, i);
+    if (kBatch) {
+        rbox.write(lds.box);
+        ritem.write(lds.item);
+        rheal.write(lds.heal);
+        rzone.write(lds.zone);
+    }
     V.ag(0, i) = g.c.x;
     V.ag(1, i) = g.c.y;
     V.ag(2, i) = g.a;
@@ -1068,10 +1141,10 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
         const uint32_t sb = slot_mask<C>(valid && bchanged);
         const uint32_t si = slot_mask<C>(valid && (dirty_env & kGItem));
         const uint32_t sh = slot_mask<C>(valid && (dirty_env & kGHeal));
-        if (sb) slot_store<S>(lds.box, state, N, lds.eidx, LY::box, LY::kBoxW, sb);
-        if (si) slot_store<S>(lds.item, state, N, lds.eidx, LY::item, LY::kItemW, si);
-        if (sh) slot_store<S>(lds.heal, state, N, lds.eidx, LY::heal, LY::kHealW, sh);
-        if (sv) slot_store<S>(lds.zone, state, N, lds.eidx, LY::zone, LY::kZoneW, sv);
+        if (sb) slot_store<S, LY::kBoxW>(lds.box, state, N, lds.eidx, LY::box, sb);
+        if (si) slot_store<S, LY::kItemW>(lds.item, state, N, lds.eidx, LY::item, si);
+        if (sh) slot_store<S, LY::kHealW>(lds.heal, state, N, lds.eidx, LY::heal, sh);
+        if (sv) slot_store<S, LY::kZoneW>(lds.zone, state, N, lds.eidx, LY::zone, sv);
     }
     // ---------------- auto-reset list: the done envs ----------------
     if (ar) {
