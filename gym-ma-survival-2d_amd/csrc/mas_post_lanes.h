@@ -540,18 +540,29 @@ struct SeqRow {
     }
 };
 
-template <class C>
+// EX: the config fills the class exactly (A, B, H at the class maxima, no
+// lasers) with Teams = P.teams: every count is a compile-time constant, so
+// the whole row unrolls and each column's index -- the sink's buffer slot and
+// store offset -- is known at compile time (no per-column branch tree).
+// Otherwise the counts come from P.  Either way every lane makes the same
+// puts in the same order (the other agents by rank), so the column index is
+// wave-uniform.
+template <class C, bool EX, bool TEAMS>
 __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Params& P, uint32_t alive_m, int i,
                                                   int lastmeta, float lhx, float lhy, SeqRow& o)
 {
     using PV = PostV<C>;
-    const int A = P.A;
+    const int A = EX ? C::AM : P.A;
+    const int B = EX ? C::BM : P.B;
+    const int H = EX ? C::HM : P.H;
+    const int NL = EX ? 0 : P.n_lasers;
+    const bool teams = EX ? TEAMS : (P.teams != 0);
     const bool alive = bit(alive_m, i);
     const int pp = __popc(alive_m & ((1u << i) - 1u));  // post-despawn list position (quirk D1)
     auto agent_row = [&](int k) {
         const bool ak = bit(alive_m, k);
         o.put((float)k);
-        if (P.teams) o.put((float)team_of(P, k));
+        if (teams) o.put((float)team_of(P, k));
         o.put(ak ? V.ag(6, k) : 0.0f);
 #pragma unroll
         for (int f = 0; f < 6; ++f) o.put(ak ? V.ag(f, k) : 0.0f);
@@ -562,10 +573,11 @@ __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Param
     };
     // agent
     agent_row(i);
-    if (P.B > 0) {
+    if (B > 0) {
         // box_items, box_items_mask
         const int ni = V.nbi();
-        for (int b = 0; b < P.B; ++b) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
             const bool present = b < ni;
             const float hx = V.ihx(b), hy = V.ihy(b);
             const int rot = bi_rot(V.imeta(b));
@@ -579,7 +591,8 @@ __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Param
             o.put(present ? ip.x : 0.0f);
             o.put(present ? ip.y : 0.0f);
         }
-        for (int b = 0; b < P.B; ++b) o.put(seen_mask(b < ni, BIdx<C>::bitem + b));
+#pragma unroll
+        for (int b = 0; b < B; ++b) o.put(seen_mask(b < ni, BIdx<C>::bitem + b));
         // box_slot, box_slot_mask
         const bool isbox = it_kind(lastmeta) == kItemBox;
 #pragma unroll
@@ -591,7 +604,8 @@ __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Param
         o.put(isbox ? 0.0f : 1.0f);
         // boxes, boxes_mask
         const int nb = V.nbox();
-        for (int b = 0; b < P.B; ++b) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
             const bool present = b < nb;
             const int meta = V.bmeta(b);
             const Poly4 poly = box_poly(V.bhx(b), V.bhy(b), box_rot(meta), box_copied(meta));
@@ -605,30 +619,35 @@ __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Param
             o.put(present ? bp.y : 0.0f);
             o.put(0.0f);  // box bodies always have angle 0
         }
-        for (int b = 0; b < P.B; ++b) o.put(seen_mask(b < nb, BIdx<C>::box + b));
+#pragma unroll
+        for (int b = 0; b < B; ++b) o.put(seen_mask(b < nb, BIdx<C>::box + b));
     }
-    if (P.H > 0) {
+    if (H > 0) {
         // heal_slot, heal_slot_mask
         const bool isheal = it_kind(lastmeta) == kItemHeal;
         o.put(isheal ? (float)P.healing : 0.0f);
         o.put(isheal ? 0.0f : 1.0f);
         // heals, heals_mask
         const int nh = V.nheal();
-        for (int h = 0; h < P.H; ++h) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
             const bool present = h < nh;
             const V2 hp = V.hp(h);
             o.put(present ? hp.x : 0.0f);
             o.put(present ? hp.y : 0.0f);
         }
-        for (int h = 0; h < P.H; ++h) o.put(seen_mask(h < nh, BIdx<C>::heal + h));
+#pragma unroll
+        for (int h = 0; h < H; ++h) o.put(seen_mask(h < nh, BIdx<C>::heal + h));
     }
     // lidars: zeros here; k_lidar writes the columns afterwards
-    for (int k = 0; k < P.n_lasers; ++k) o.put(0.0f);
-    // others, others_mask (the seen list at the post-despawn list index)
-    for (int k = 0; k < A; ++k)
-        if (k != i) agent_row(k);
-    for (int k = 0; k < A; ++k) {
-        if (k == i) continue;
+    for (int k = 0; k < NL; ++k) o.put(0.0f);
+    // others, others_mask: the other agents by rank (agent k skips i), the
+    // seen list at the post-despawn list index
+#pragma unroll
+    for (int r = 0; r + 1 < A; ++r) agent_row(r < i ? r : r + 1);
+#pragma unroll
+    for (int r = 0; r + 1 < A; ++r) {
+        const int k = r < i ? r : r + 1;
         const bool ak = bit(alive_m, k);
         o.put((alive && ak && ((V.sn(BIdx<C>::agent + k) >> pp) & 1u)) ? 0.0f : 1.0f);
     }
@@ -1182,7 +1201,10 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
         const uintptr_t ob = reinterpret_cast<uintptr_t>(obs);
         const int vm1 = (D & 3) == 0 && (ob & 15) == 0 ? 3 : ((D & 1) == 0 && (ob & 7) == 0 ? 1 : 0);
         SeqRow o{obs + (e * A + i) * (int64_t)D, vm1};
-        write_obs_row_seq<C>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+        const bool ex = A == C::AM && P.B == C::BM && P.H == C::HM && P.n_lasers == 0;
+        if (ex && P.teams) write_obs_row_seq<C, true, true>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+        else if (ex) write_obs_row_seq<C, true, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+        else write_obs_row_seq<C, false, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
     }
 #else
     const int trow = j * A + i;  // tile row (the wave's rows are consecutive unless kGenEnvs)
