@@ -1111,13 +1111,18 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
         if (valid && i == 0) {
             done[e] = is_done ? 1 : 0;
             float* st = reinterpret_cast<float*>(state);
+            // every word's load issued before any add (the per-word
+            // read-modify-write under q < R waited out one load latency each)
+            float cur[17];
+#pragma unroll
+            for (int q = 0; q < 17; ++q) cur[q] = st[state_index(LY::stat + q, e, N)];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 if (q >= R) continue;
-                st[state_index(LY::stat + q, e, N)] += rq[q];
-                st[state_index(LY::stat + 8 + q, e, N)] += (float)kq[q];
+                st[state_index(LY::stat + q, e, N)] = cur[q] + rq[q];
+                st[state_index(LY::stat + 8 + q, e, N)] = cur[8 + q] + (float)kq[q];
             }
-            st[state_index(LY::stat + 16, e, N)] += 1.0f;
+            st[state_index(LY::stat + 16, e, N)] = cur[16] + 1.0f;
         }
     }
     MAS_PROF(P, 43);
