@@ -538,6 +538,53 @@ struct SeqRow {
         }
         ++k;
     }
+    __device__ __forceinline__ void finish() {}
+};
+
+// The four rows of an env through LDS (A == C::AM == 4, D % 4 == 0, the
+// compile-time column layout): each lane buffers 16 consecutive columns of its
+// own row; at every 16-column boundary the env's four lanes swap them through
+// LDS so that each store instruction writes one 64-B run of ONE row per env
+// (lane i: floats 4i..4i+3 of the run) instead of 16 B of every lane's row --
+// the 16-B pieces made the L2 write back partial 64-B halves (k_post_lanes
+// WRITE_SIZE 295 vs 196 MB per 2v2 step, r04i vs r04e).  With the layout known
+// at compile time every buffer slot and flush point is a constant (the same
+// sink over run-time counts doubled the kernel's code).  stg: the env slot's
+// [4 rows][4 float4] in LDS; every lane of the env calls it (on: store).
+struct QuadRow {
+    float* env;   // obs row 0 of the env
+    float4* stg;  // LDS staging of the slot
+    int i, D;     // this lane's row; the row length
+    bool on;      // the env's rows are stored
+    int k = 0;    // next column
+    float b[16];
+    __device__ __forceinline__ void put(float v)
+    {
+        const int s = k & 15;
+        // (constant indices only: b stays in registers; s is a constant here)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (s == q) b[q] = v;
+        if (s == 15) flush(k - 15, 16);
+        ++k;
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if ((k & 15) != 0) flush(k - (k & 15), k & 15);
+    }
+    __device__ __forceinline__ void flush(int g0, int n)
+    {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * q < n) stg[i * 4 + q] = make_float4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+        // (one wave: its LDS writes precede its reads, the previous group's
+        // reads precede these writes)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float4 v = stg[r * 4 + i];
+            if (on && 4 * i < n) *reinterpret_cast<float4*>(env + (int64_t)r * D + g0 + 4 * i) = v;
+        }
+    }
 };
 
 // EX: the config fills the class exactly (A, B, H at the class maxima, no
@@ -547,9 +594,9 @@ struct SeqRow {
 // Otherwise the counts come from P.  Either way every lane makes the same
 // puts in the same order (the other agents by rank), so the column index is
 // wave-uniform.
-template <class C, bool EX, bool TEAMS>
+template <class C, bool EX, bool TEAMS, class Sink>
 __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Params& P, uint32_t alive_m, int i,
-                                                  int lastmeta, float lhx, float lhy, SeqRow& o)
+                                                  int lastmeta, float lhx, float lhy, Sink& o)
 {
     using PV = PostV<C>;
     const int A = EX ? C::AM : P.A;
@@ -668,6 +715,7 @@ __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Param
     o.put(z3);
     o.put(z4);
     o.put(z5);
+    o.finish();
 }
 
 // The post-physics phases of one step on agent lanes (see the file comment),
@@ -1200,13 +1248,19 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
     const int D = P.D;
     const bool row_on = valid && i < A;
 #if MAS_POST_OBS_SEQ
-    if (row_on) {
+    const uintptr_t ob = reinterpret_cast<uintptr_t>(obs);
+    const bool ex = A == C::AM && P.B == C::BM && P.H == C::HM && P.n_lasers == 0;
+    if (C::AM == 4 && ex && (D & 3) == 0 && (ob & 15) == 0) {
+        // every lane (the swaps need the env's four), stores by `valid`
+        static_assert(C::AM != 4 || sizeof(lds.u) >= sizeof(float4) * 16 * S, "the staging fits the union");
+        QuadRow o{obs + e * (int64_t)(A * D), reinterpret_cast<float4*>(&lds.u) + j * 16, i, D, valid};
+        if (P.teams) write_obs_row_seq<C, true, true>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+        else write_obs_row_seq<C, true, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+    } else if (row_on) {
         // 16-B stores when the rows are 16-B aligned (D % 4 == 0 and a 16-B
         // aligned buffer), else 8-B / 4-B
-        const uintptr_t ob = reinterpret_cast<uintptr_t>(obs);
         const int vm1 = (D & 3) == 0 && (ob & 15) == 0 ? 3 : ((D & 1) == 0 && (ob & 7) == 0 ? 1 : 0);
         SeqRow o{obs + (e * A + i) * (int64_t)D, vm1};
-        const bool ex = A == C::AM && P.B == C::BM && P.H == C::HM && P.n_lasers == 0;
         if (ex && P.teams) write_obs_row_seq<C, true, true>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
         else if (ex) write_obs_row_seq<C, true, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
         else write_obs_row_seq<C, false, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
