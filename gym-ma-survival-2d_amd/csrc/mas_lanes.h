@@ -597,10 +597,18 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
             const float dd = len(sub(c, oc));
             if (dd < mind) { mind = dd; best = id; }
         };
+        // (over the class maxima, the counts as guards: the LDS reads up front;
+        // the same bodies in the same order)
         const int nb = V.nbox(), ni = V.nbi(), nh = V.nheal();
-        for (int b = 0; b < nb; ++b) consider(V.bp(b), BIdx<C>::box + b);
-        for (int b = 0; b < ni; ++b) consider(V.ip(b), BIdx<C>::bitem + b);
-        for (int h = 0; h < nh; ++h) consider(V.hp(h), BIdx<C>::heal + h);
+#pragma unroll
+        for (int b = 0; b < C::BM; ++b)
+            if (b < nb) consider(V.bp(b), BIdx<C>::box + b);
+#pragma unroll
+        for (int b = 0; b < C::BM; ++b)
+            if (b < ni) consider(V.ip(b), BIdx<C>::bitem + b);
+#pragma unroll
+        for (int h = 0; h < C::HM; ++h)
+            if (h < nh) consider(V.hp(h), BIdx<C>::heal + h);
 #pragma unroll
         for (int w = 0; w < kNumWalls; ++w) consider(P.wall_pos[w], BIdx<C>::wall + w);
         const uint32_t alive_m = alive_m0;

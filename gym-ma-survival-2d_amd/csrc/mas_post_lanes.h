@@ -202,14 +202,18 @@ __device__ __forceinline__ int ray_cast_pv(const Params& P, const PostV<C>& V, u
         if (c.x - ex > hix || c.x + ex < lox || c.y - ey > hiy || c.y + ey < loy) return false;
         return fabsf(dot(v, sub(p1, c))) - (av.x * ex + av.y * ey) <= m;
     };
+    // (over the class maxima with the counts as guards: every LDS read of the
+    // cull issued up front instead of one loop round trip per body)
     const int nbox = V.nbox(), nbi = V.nbi(), nheal = V.nheal();
     uint64_t mask = 0;
-    for (int b = 0; b < nbox; ++b)
-        if (keep(V.bp(b), V.bhx(b), V.bhy(b))) mask |= 1ull << (BIdx<C>::box + b);
-    for (int b = 0; b < nbi; ++b)
-        if (keep(V.ip(b), P.bitem_r, P.bitem_r)) mask |= 1ull << (BIdx<C>::bitem + b);
-    for (int h = 0; h < nheal; ++h)
-        if (keep(V.hp(h), P.heal_r, P.heal_r)) mask |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (b < nbox && keep(V.bp(b), V.bhx(b), V.bhy(b))) mask |= 1ull << (BIdx<C>::box + b);
+        if (b < nbi && keep(V.ip(b), P.bitem_r, P.bitem_r)) mask |= 1ull << (BIdx<C>::bitem + b);
+    }
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h)
+        if (h < nheal && keep(V.hp(h), P.heal_r, P.heal_r)) mask |= 1ull << (BIdx<C>::heal + h);
 #pragma unroll
     for (int w = 0; w < kNumWalls; ++w) {
         const V2 c = scl(0.5f, add(P.wall_lo[w], P.wall_hi[w]));
@@ -276,7 +280,9 @@ __device__ __forceinline__ bool box_health_v(const PostV<C>& V, const Params& P,
     any_dead = false;
     kept = 0;
     nb = V.nbox();
-    for (int b = 0; b < nb; ++b) {
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        if (b >= nb) continue;
         const int meta = V.bmeta(b);
         if (!box_hinit(meta)) {
             V.bw(5 + 6 * b) = (uint32_t)mk_boxmeta(box_rot(meta), box_copied(meta), 1, box_vuln(meta), box_cause(meta));
@@ -847,12 +853,14 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
             const V2 pos = g.c;
             const Rot q = rot_of(g.a);
             const int nb = V.nbox(), ni = V.nbi(), nh = V.nheal();
-            for (int b = 0; b < nb; ++b)
-                if (poly_test_point(P.cone, pos, q, V.bp(b))) cand |= 1ull << (BIdx<C>::box + b);
-            for (int b = 0; b < ni; ++b)
-                if (poly_test_point(P.cone, pos, q, V.ip(b))) cand |= 1ull << (BIdx<C>::bitem + b);
-            for (int h = 0; h < nh; ++h)
-                if (poly_test_point(P.cone, pos, q, V.hp(h))) cand |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b) {
+                if (b < nb && poly_test_point(P.cone, pos, q, V.bp(b))) cand |= 1ull << (BIdx<C>::box + b);
+                if (b < ni && poly_test_point(P.cone, pos, q, V.ip(b))) cand |= 1ull << (BIdx<C>::bitem + b);
+            }
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h)
+                if (h < nh && poly_test_point(P.cone, pos, q, V.hp(h))) cand |= 1ull << (BIdx<C>::heal + h);
 #pragma unroll
             for (int w = 0; w < kNumWalls; ++w)
                 if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) cand |= 1ull << (BIdx<C>::wall + w);
@@ -1017,10 +1025,12 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
         uint32_t lb = 0, lh = 0;
         if (alive) {
             const int ni = V.nbi(), nh = V.nheal();
-            for (int b = 0; b < ni; ++b)
-                if (circle_test_point(P.pickup_r, g.c, V.ip(b))) lb |= 1u << b;
-            for (int h = 0; h < nh; ++h)
-                if (circle_test_point(P.pickup_r, g.c, V.hp(h))) lh |= 1u << h;
+#pragma unroll
+            for (int b = 0; b < C::BM; ++b)
+                if (b < ni && circle_test_point(P.pickup_r, g.c, V.ip(b))) lb |= 1u << b;
+#pragma unroll
+            for (int h = 0; h < C::HM; ++h)
+                if (h < nh && circle_test_point(P.pickup_r, g.c, V.hp(h))) lh |= 1u << h;
         }
         uint32_t takenb = 0, takenh = 0;
         while (lb) {
