@@ -616,8 +616,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
 int mas_destroy(mas_handle* h)
 {
     if (!h) return MAS_OK;
-    if (h->state) hipFree(h->state);
-    if (h->seedbuf) hipFree(h->seedbuf);
+    if (h->state) (void)hipFree(h->state);
+    if (h->seedbuf) (void)hipFree(h->seedbuf);
     if (h->P.prof) (void)hipFree(h->P.prof);
     if (h->phys) (void)hipFree(h->phys);
     if (h->sweep) (void)hipFree(h->sweep);
