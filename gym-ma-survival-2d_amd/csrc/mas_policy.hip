@@ -409,57 +409,6 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
 constexpr int kHeadN[6] = {3, 3, 3, 2, 2, 2};
 constexpr int kHeadOff[6] = {0, 3, 6, 9, 11, 13};
 
-// the rollout outputs of one row (lane half 0) from its layer-3 accumulator:
-// Gumbel-max sampling of the six heads, log-prob, value
-__device__ __forceinline__ void act_outputs(const f16v& z3, const float* __restrict__ b3, uint64_t seed, uint64_t step,
-                                            int64_t first_row, int64_t row, int8_t* __restrict__ act,
-                                            float* __restrict__ logp, float* __restrict__ value)
-{
-    float z[kO];
-#pragma unroll
-    for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
-    // Gumbel-max over each head; the RNG stream of k_sample (mas_capi.hip),
-    // hardware exp2/log2 (the draws agree with k_sample up to ~1 ulp ties)
-    // (keyed by the row's index in the whole batch: a shard launched with its
-    // first_row draws what the unsharded launch draws for those rows)
-    const uint64_t base = mix64(seed ^ mix64(step * 0x100000001B3ULL + (uint64_t)(first_row + row)));
-    float lp = 0.0f;
-    uint32_t packed_a[2] = {0u, 0u};
-#pragma unroll
-    for (int hd = 0; hd < 6; ++hd) {
-        const int n = kHeadN[hd], off = kHeadOff[hd];
-        float mx = z[off];
-#pragma unroll
-        for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
-        float se = 0.0f;
-#pragma unroll
-        for (int k = 0; k < n; ++k) se += exp_fast(z[off + k] - mx);
-        const float lse = mx + log_fast(se);
-        int best = 0;
-        float bv = -INFINITY, lb = z[off];
-#pragma unroll
-        for (int k = 0; k < n; ++k) {
-            const uint64_t r = mix64(base + (uint64_t)(hd * 4 + k));
-            const float u = ((float)(r >> 40) + 0.5f) * (1.0f / 16777216.0f);
-            const float g = z[off + k] - log_fast(-log_fast(u));
-            if (g > bv) {
-                bv = g;
-                best = k;
-                lb = z[off + k];
-            }
-        }
-        lp += lb - lse;
-        packed_a[hd >> 2] |= (uint32_t)best << (8 * (hd & 3));
-    }
-    // 6 int8 per row (2-B aligned): three 2-B stores
-    uint16_t* ap = reinterpret_cast<uint16_t*>(act + row * 6);
-    ap[0] = (uint16_t)packed_a[0];
-    ap[1] = (uint16_t)(packed_a[0] >> 16);
-    ap[2] = (uint16_t)packed_a[1];
-    logp[row] = lp;
-    value[row] = z[kO - 1];
-}
-
 // KS > 0: compile-time k-step count (obs_dim in (16 (KS-1), 16 KS]) with every
 // x fragment loaded up front; KS == 0: any obs_dim, chunked layer 1
 template <int KS>
@@ -518,7 +467,50 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
         value[row] = z3[0] + z3[15];
         return;
     }
-    act_outputs(z3, B1 + 2 * kMT * 2 * 16, seed, step, first_row, row, act, logp, value);
+    float z[kO];
+    const float* b3 = B1 + 2 * kMT * 2 * 16;
+#pragma unroll
+    for (int o = 0; o < kO; ++o) z[o] = z3[o] + b3[o];
+    // Gumbel-max over each head; the RNG stream of k_sample (mas_capi.hip),
+    // hardware exp2/log2 (the draws agree with k_sample up to ~1 ulp ties)
+    // (keyed by the row's index in the whole batch: a shard launched with its
+    // first_row draws what the unsharded launch draws for those rows)
+    const uint64_t base = mix64(seed ^ mix64(step * 0x100000001B3ULL + (uint64_t)(first_row + row)));
+    float lp = 0.0f;
+    uint32_t packed_a[2] = {0u, 0u};
+#pragma unroll
+    for (int hd = 0; hd < 6; ++hd) {
+        const int n = kHeadN[hd], off = kHeadOff[hd];
+        float mx = z[off];
+#pragma unroll
+        for (int k = 1; k < n; ++k) mx = fmaxf(mx, z[off + k]);
+        float se = 0.0f;
+#pragma unroll
+        for (int k = 0; k < n; ++k) se += exp_fast(z[off + k] - mx);
+        const float lse = mx + log_fast(se);
+        int best = 0;
+        float bv = -INFINITY, lb = z[off];
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+            const uint64_t r = mix64(base + (uint64_t)(hd * 4 + k));
+            const float u = ((float)(r >> 40) + 0.5f) * (1.0f / 16777216.0f);
+            const float g = z[off + k] - log_fast(-log_fast(u));
+            if (g > bv) {
+                bv = g;
+                best = k;
+                lb = z[off + k];
+            }
+        }
+        lp += lb - lse;
+        packed_a[hd >> 2] |= (uint32_t)best << (8 * (hd & 3));
+    }
+    // 6 int8 per row (2-B aligned): three 2-B stores
+    uint16_t* ap = reinterpret_cast<uint16_t*>(act + row * 6);
+    ap[0] = (uint16_t)packed_a[0];
+    ap[1] = (uint16_t)(packed_a[0] >> 16);
+    ap[2] = (uint16_t)packed_a[1];
+    logp[row] = lp;
+    value[row] = z[kO - 1];
 }
 
 struct TrainArgs {
@@ -1173,57 +1165,9 @@ __device__ __forceinline__ void land_db()
     lds_barrier();
 }
 
-// Transposed activation stores (TR, needs ld % 4 == 0): the MFMA C layout
-// gives lane (r, h) row r of 16 features; a 32x32x16 MFMA of that fragment
-// (as the A operand: m = row, k = feature) with a permutation matrix as B
-// (B[k][n] = 1 where register k holds feature n) yields the same 32 x 32 tile
-// transposed -- lane (n, h) then holds feature n for rows 4 h + 8 q + i --
-// so each lane stores four runs of four consecutive rows of one feature
-// (8-B stores, 4 per tile) where store_rows2 pairs rows through a DPP swap
-// (6-7 VALU and one 4-B store per pair, 8 per tile).  Exact: one product
-// x * 1 per output, the rest x * 0 (a -0 comes out +0; the tile's values are
-// finite).
-__device__ __forceinline__ void ident_frags(int l, bf8 (&id)[2])
-{
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    const int n = l & 31, h = l >> 5;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        // register j of fragment c holds feature 16 c + 8 (j >> 2) + 4 h + (j & 3) (crow)
-        const int d = n - 16 * c - 4 * h;
-        const bool ok = (d >= 0 && d < 4) || (d >= 8 && d < 12);
-        const int js = (d & 3) + 4 * ((d >> 3) & 1);
-        u4 w;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = (ok && (js >> 1) == k) ? (0x3F80u << (16 * (js & 1))) : 0u;
-        id[c] = __builtin_bit_cast(bf8, w);
-    }
-}
-__device__ __forceinline__ void store_tr(__bf16* base, int64_t M, int64_t row, int mt, int h, const bf8 (&v)[2],
-                                         const bf8 (&id)[2])
-{
-    f16v c = f16v{};
-    c = mfma(v[0], id[0], c);
-    c = mfma(v[1], id[1], c);
-    const uint32_t m2 = __builtin_amdgcn_readfirstlane((uint32_t)(M * 2));
-    // lane (n, h): feature 32 mt + n, rows (row & ~31) + 4 h + 8 q + i
-    const uint32_t lane_off = (uint32_t)(row & 31) * m2 + (uint32_t)((row & ~(int64_t)31) + 4 * h) * 2u;
-    uint8_t* p = reinterpret_cast<uint8_t*>(base) + (lane_off + (uint32_t)(32 * mt) * m2);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        // (the values are bf16 already: their high halves, paired by one v_perm_b32)
-        uint2 o;
-        o.x = __builtin_amdgcn_perm(__float_as_uint(c[4 * q + 1]), __float_as_uint(c[4 * q]), 0x07060302u);
-        o.y = __builtin_amdgcn_perm(__float_as_uint(c[4 * q + 3]), __float_as_uint(c[4 * q + 2]), 0x07060302u);
-        *reinterpret_cast<uint2*>(p + 16 * q) = o;
-    }
-}
-
-template <int KS, bool OFF32, bool TR>
+template <int KS, bool OFF32>
 __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, int64_t nblk)
 {
-    static_assert(!TR || OFF32, "the transposed stores use 32-bit offsets");
-    constexpr int kSt = TR ? 4 : 8;  // vector stores per activation tile
     static_assert(KS > 0, "compile-time layer-1 depth");
     constexpr int NCH = (KS + kKc - 1) / kKc;  // layer-1 stages
     __shared__ bf8 wl[2 * kLdsFrag];
@@ -1243,15 +1187,11 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
     auto buf = [&](int k) { return wl + (k & 1) * kLdsFrag; };
     // (each tile's 8 stores fenced off from the scheduler: a burst of
     // interleaved tiles' pair shuffles would spill)
-    bf8 idf[2];  // TR: the permutation fragments (ident_frags)
     auto st2 = [&](__bf16* base, int64_t row, int t, int h, const bf8 (&v)[2]) {
         // (row re-materialised per tile: CSE'd across the buffers, the 64
         // per-word store offsets stayed live from phase C to G and spilled)
         asm volatile("" : "+v"(row));
-        if constexpr (TR)
-            store_tr(base, LD, row, t, h, v, idf);
-        else
-            store_rows2<OFF32>(base, LD, row, t, h, v);
+        store_rows2<OFF32>(base, LD, row, t, h, v);
 #if MAS_POL_DB_SB
         __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -1266,7 +1206,6 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
         asm volatile("" : "+v"(l));
         const int h = l >> 5;
         const int64_t row = blk * kDRows + wv * 32 + (l & 31);
-        if constexpr (TR) ident_frags(l, idf);  // from the opaque lane index: rebuilt per block
         bf8 h1[kMT][2], h2[kMT][2];
         // the loss inputs of the row (read in phase E)
         uint32_t aw0 = 0, aw1 = 0;  // the row's 6 action bytes: 0..3, 4..5
@@ -1281,7 +1220,7 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
             for (int c = 0; c < NCH; ++c) {
                 if (c == 0) {
                     if (blk == b0) land_db<0>();   // the prologue's copies
-                    else land_db<4 * kSt>();       // phase G: 32 dA1 stores after them (4 tiles)
+                    else land_db<32>();            // phase G: 32 dA1 stores after them
                 } else {
                     if (c == 1) land_db<KS>();  // chunk 0: the x loads after them
                     else land_db<0>();
@@ -1314,7 +1253,7 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             if (hf == 0) land_db<NCH == 1 ? KS : 0>();
-            else land_db<8 * kSt>();  // phase C: the 8 h1 tiles' stores after them
+            else land_db<64>();  // phase C: 64 h1 stores after them
             const bf8* wl2 = buf(sc);
             if (hf == 0) {
                 copy_db(buf(sc + 1), F + Lo.w23() + kHalf * 64, kHalf * 64);
@@ -1358,7 +1297,7 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
         // (in-out operands: nothing derived from them is computed before)
         asm volatile("" : "+v"(aw0), "+v"(aw1), "+v"(adv), "+v"(old_lp), "+v"(ret)::"memory");
         // ---- E: W3^T; the loss gradient, dA2
-        land_db<6 + 4 * kSt>();  // phase D: 6 loss-input loads + 4 h2 tiles' stores after them
+        land_db<38>();  // phase D: 6 loss-input loads + 32 h2 stores after them
         const bf8* wb = buf(sc);
         copy_db(buf(sc + 1), F + Lo.wbk() + kBk0 * 64, kBk1 * 64);
 #pragma unroll
@@ -1446,8 +1385,8 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
         // ---- F, G: W2^T halves; dA1
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
-            if (hf == 0) land_db<12 * kSt>();  // phase E: 4 h2 + 8 dA2 tiles' stores (+ 16 dz) after them
-            else land_db<4 * kSt>();     // phase F: 4 dA1 tiles' stores
+            if (hf == 0) land_db<96>();  // phase E: 32 h2 + 64 dA2 stores (+ 16 dz) after them
+            else land_db<32>();          // phase F: 32 dA1 stores
             const bf8* W2T = buf(sc);
             if (hf == 0) copy_db(buf(sc + 1), F + Lo.wbk() + (kBk0 + kBk1) * 64, kBk1 * 64);
             else if (blk + gridDim.x < nblk) copy_db(buf(sc + 1), F + Lo.w1(), (KS < kKc ? KS : kKc) * kMT * 64);
@@ -1489,120 +1428,6 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
             }
             A.partials[(2 * blk + (threadIdx.x >> 2)) * 4 + k] = v;
         }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_policy_act_db: the rollout's policy forward + sampling in the form of
-// k_policy_train_db -- one persistent 8-wave workgroup per CU over 256-row
-// blocks, the weight stages double-buffered (the copies of stage p + 1 issued
-// at the start of phase p, landing with counted waits) -- where
-// k_policy_act runs two 4-wave workgroups per CU, each staging and draining
-// every weight stage for its 128 rows behind two barriers.  Phases per block:
-// W1 chunks (NCH), then the two W2+W3 half stages; the next block's first W1
-// chunk is copied during the last.  Full 256-row blocks with D = 16 KS (the
-// x loads branch-free: 2 per k-step, the count the second chunk's landing
-// waits with); the rest on k_policy_act.  Same operations per row as
-// k_policy_act: bit-identical outputs (test_act_db_kernel_is_bit_identical).
-template <int KS>
-__global__ __launch_bounds__(64 * kDW, 1) void k_policy_act_db(const uint8_t* __restrict__ packed, int D, int64_t nblk,
-                                                               const float* __restrict__ obs, __bf16* __restrict__ xb,
-                                                               int64_t xb_stride, uint64_t seed, uint64_t step,
-                                                               int64_t first_row, int8_t* __restrict__ act,
-                                                               float* __restrict__ logp, float* __restrict__ value)
-{
-    static_assert(KS > 0, "compile-time layer-1 depth");
-    constexpr int NCH = (KS + kKc - 1) / kKc;  // layer-1 stages
-    __shared__ bf8 wl[2 * kLdsFrag];
-    __shared__ float bl[kBiasF];
-    const Layout Lo{KS};
-    const bf8* F = reinterpret_cast<const bf8*>(packed);
-    const float* FB = reinterpret_cast<const float*>(packed);
-    bias_lds(bl, FB + Lo.b1());
-    const float* b1p = bl;
-    const float* b2p = bl + kMT * 2 * 16;
-    const float* b3 = bl + 2 * kMT * 2 * 16;
-    const int l0 = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int sc = 0;  // stages so far: the current one is in buffer sc & 1
-    auto buf = [&](int k) { return wl + (k & 1) * kLdsFrag; };
-    const int64_t b0 = blockIdx.x;
-    if (b0 < nblk) copy_db(buf(0), F + Lo.w1(), (KS < kKc ? KS : kKc) * kMT * 64);  // prologue
-    for (int64_t blk = b0; blk < nblk; blk += gridDim.x) {
-        int l = l0;
-        asm volatile("" : "+v"(l));  // (as in k_policy_train_db: no hoisted per-block addresses)
-        const int h = l >> 5;
-        const int64_t row = blk * kDRows + wv * 32 + (l & 31);
-        bf8 h1[kMT][2];
-        // ---- layer 1: NCH stages of up to kKc k-steps
-        {
-            f16v acc[kMT];
-#pragma unroll
-            for (int mt = 0; mt < kMT; ++mt) acc[mt] = f16v{};
-            bf8 x[KS];
-#pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-                if (c == 0) {
-                    if (blk == b0) land_db<0>();  // the prologue's copies
-                    else land_db<3>();            // the previous block's outputs: at least 3 stores after them
-                } else {
-                    if (c == 1) land_db<2 * KS>();  // chunk 0: the 2 KS x loads after them
-                    else land_db<0>();
-                }
-                const bf8* w = buf(sc);
-                if (c + 1 < NCH) {
-                    const int k1 = (c + 1) * kKc, kn = KS - k1 < kKc ? KS - k1 : kKc;
-                    copy_db(buf(sc + 1), F + Lo.w1() + k1 * kMT * 64, kn * kMT * 64);
-                } else {
-                    copy_db(buf(sc + 1), F + Lo.w23(), kHalf * 64);
-                }
-                if (c == 0) {
-#pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) x[ks] = x_frag_f32_full(obs, row, true, D, 16 * ks + 8 * h);
-                    if (xb != nullptr) {
-#pragma unroll
-                        for (int ks = 0; ks < KS; ++ks)
-                            *reinterpret_cast<bf8*>(xb + row * xb_stride + 16 * ks + 8 * h) = x[ks];
-                    }
-                }
-                const int kn = KS - c * kKc < kKc ? KS - c * kKc : kKc;
-#pragma unroll
-                for (int q = 0; q < kn; ++q) {
-                    const bf8* wk = w + q * kMT * 64 + l;
-#pragma unroll
-                    for (int mt = 0; mt < kMT; ++mt) acc[mt] = mfma(wk[mt * 64], x[c * kKc + q], acc[mt]);
-                }
-                ++sc;
-            }
-            tanh_h1(acc, b1p, h, h1);
-        }
-        // ---- layers 2 + 3: two half stages
-        f16v z3 = f16v{};
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            if (hf == 0) land_db<NCH == 1 ? 2 * KS : 0>();
-            else land_db<0>();
-            const bf8* wl2 = buf(sc);
-            if (hf == 0) copy_db(buf(sc + 1), F + Lo.w23() + kHalf * 64, kHalf * 64);
-            else if (blk + gridDim.x < nblk) copy_db(buf(sc + 1), F + Lo.w1(), (KS < kKc ? KS : kKc) * kMT * 64);
-#pragma unroll
-            for (int q = 0; q < kMT / 2; ++q) {
-                const int mo = kMT / 2 * hf + q;
-                f16v a = f16v{};
-                const bf8* w = wl2 + q * 16 * 64 + l;
-#pragma unroll
-                for (int kk = 0; kk < 16; ++kk) a = mfma(w[kk * 64], h1[kk >> 1][kk & 1], a);
-                float b[16];
-                load16(b2p + (mo * 2 + h) * 16, b);
-                bf8 f[2];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) f[i >> 3][i & 7] = (__bf16)tanh_pre(a[i], b[i]);
-                const bf8* w3 = wl2 + (kMT / 2 * 16 + 2 * q) * 64 + l;
-                z3 = mfma(w3[0], f[0], z3);
-                z3 = mfma(w3[64], f[1], z3);
-            }
-            ++sc;
-        }
-        if (h == 0) act_outputs(z3, b3, seed, step, first_row, row, act, logp, value);
     }
 }
 
@@ -1985,31 +1810,9 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
                       hipStream_t s)
 {
     const int ks1 = (D + 15) / 16;
-    // the persistent double-buffered kernel for the full 256-row blocks when
-    // obs_dim fills its k-steps (D = 16 ks1, ks1 9 or 10), k_policy_act for
-    // the rest; MAS_POL_ACT_DB=1 (read per call) selects it
-    const char* adb = getenv("MAS_POL_ACT_DB");
-    const int64_t nfull = M / pol::kDRows;
-    int64_t r0 = 0;
-    if ((ks1 == 10 || ks1 == 9) && D == 16 * ks1 && nfull > 0 && adb && adb[0] == '1') {
-        static int ncu = 0;
-        if (ncu == 0) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-                ncu = 256;
-        }
-        const int64_t grid = nfull < ncu ? nfull : ncu;
-        auto kd = ks1 == 10 ? pol::k_policy_act_db<10> : pol::k_policy_act_db<9>;
-        hipLaunchKernelGGL(kd, dim3((unsigned)grid), dim3(64 * pol::kDW), 0, s, (const uint8_t*)packed, D, nfull, obs,
-                           (__bf16*)xb, xb_stride, seed, step, first_row, act, logp, value);
-        r0 = nfull * pol::kDRows;
-        if (r0 == M) return hipGetLastError();
-    }
-    // (the rows from r0 on: offset buffers, the RNG keyed by first_row + r0)
     auto k = ks1 == 10 ? pol::k_policy_act<10> : ks1 == 9 ? pol::k_policy_act<9> : pol::k_policy_act<0>;
-    hipLaunchKernelGGL(k, dim3((unsigned)act_blocks(M - r0)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
-                       ks1, M - r0, obs + r0 * D, xb ? (__bf16*)xb + r0 * xb_stride : nullptr, xb_stride, seed, step,
-                       first_row + r0, act + r0 * 6, logp + r0, value + r0);
+    hipLaunchKernelGGL(k, dim3((unsigned)act_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
+                       ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, first_row, act, logp, value);
     return hipGetLastError();
 }
 
@@ -2057,11 +1860,7 @@ hipError_t policy_train(const void* packed, int D, int64_t M, const void* xb, in
                 ncu = 256;
         }
         const int64_t grid = nfull < ncu ? nfull : ncu;
-        // MAS_POL_TR=1: the transposed stores (else the DPP row pairs)
-        const char* tr = getenv("MAS_POL_TR");
-        const bool use_tr = (ld & 3) == 0 && tr && tr[0] == '1';
-        auto kd = A.ks1 == 10 ? (use_tr ? pol::k_policy_train_db<10, true, true> : pol::k_policy_train_db<10, true, false>)
-                              : (use_tr ? pol::k_policy_train_db<9, true, true> : pol::k_policy_train_db<9, true, false>);
+        auto kd = A.ks1 == 10 ? pol::k_policy_train_db<10, true> : pol::k_policy_train_db<9, true>;
         hipLaunchKernelGGL(kd, dim3((unsigned)grid), dim3(64 * pol::kDW), 0, s, A, nfull);
         const int64_t r0 = nfull * pol::kDRows;
         if (r0 < M) {  // the partial last block: k_policy_train on offset buffers

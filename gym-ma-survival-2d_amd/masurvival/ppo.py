@@ -363,9 +363,8 @@ class FusedPolicy:
             nb = int(self.lib.mas_policy_blocks(M))
             # h1 / h2 carry a row of ones (row 256): dW @ [h; 1]^T yields the bias gradient as its last column.
             # Row stride ld = M + _ACT_PAD: a power-of-two stride (the 4.2M-row minibatch) puts every
-            # feature row on the same HBM channels (mas_policy_train_ld); a multiple of 4: the train
-            # kernel's transposed stores write 4 rows (8 B) per lane
-            ld = ((M + 3) & ~3) + _ACT_PAD
+            # feature row on the same HBM channels (mas_policy_train_ld)
+            ld = M + _ACT_PAD
             h1, h2 = torch.empty((257, ld), **bf), torch.empty((257, ld), **bf)
             h1[256] = 1.0
             h2[256] = 1.0

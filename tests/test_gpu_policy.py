@@ -233,9 +233,8 @@ def test_fused_adam_matches_torch(max_norm, grad_scale):
     assert torch.equal(fa2.m, fa.m) and torch.equal(fa2.v, fa.v)
 
 
-@pytest.mark.parametrize('tr', ['1', '0'])
 @pytest.mark.parametrize('D,M', [(160, 8192 + 70), (138, 256 * 300 + 130), (468, 4096 + 2), (160, 128)])
-def test_counted_wait_train_kernel_is_bit_identical(D, M, tr, monkeypatch):
+def test_counted_wait_train_kernel_is_bit_identical(D, M, monkeypatch):
     """k_policy_train_db (the PPO update's default for 32-bit store offsets
     and obs_dim in (128, 160]: persistent 8-wave workgroups, double-buffered
     weight stages, full 256-row blocks; the partial last block on
@@ -245,12 +244,8 @@ def test_counted_wait_train_kernel_is_bit_identical(D, M, tr, monkeypatch):
     equal up to the order of the per-block partial sums -- full blocks plus a
     partial last block (M = 8262 and 76930: 32 / 300 full blocks + 70 / 130
     rows, D = 160 and 138: 10 and 9 layer-1 k-steps), the generic layer-1
-    k-loop (D = 468) and a single block (M = 128).  tr: the db kernel's
-    activation stores through the MFMA transpose (MAS_POL_TR=1; the row
-    stride a multiple of 4 -- FusedPolicy makes it one) or the DPP row pairs
-    (0)."""
+    k-loop (D = 468) and a single block (M = 128)."""
     monkeypatch.setattr(ppo_mod, '_POL_LAYOUT', 'fm')
-    monkeypatch.setenv('MAS_POL_TR', tr)
     cfg = PPOConfig()
     out = []
     for cw in ('1', '0'):
@@ -275,32 +270,4 @@ def test_counted_wait_train_kernel_is_bit_identical(D, M, tr, monkeypatch):
     for a, b in zip(t1, t0):
         assert abs(a - b) <= 1e-6 * max(1.0, abs(b)), (t1, t0)
     for a, b in zip(g1, g0):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize('D,M', [(160, 256 * 40 + 70), (144, 256 * 7), (160, 200)])
-def test_act_db_kernel_is_bit_identical(D, M, monkeypatch):
-    """k_policy_act_db (MAS_POL_ACT_DB=1, for obs_dim = 16 * 9 or 16 * 10:
-    persistent 8-wave workgroups, double-buffered weight stages, full 256-row
-    blocks; the rest of the rows on k_policy_act) only reorders
-    k_policy_act's copies and loads: actions, log-probs, values and the bf16
-    rows for the update are bit-identical with MAS_POL_ACT_DB=0 -- full blocks
-    plus a tail (M = 10310), full blocks only (M = 1792, D = 144: 9 k-steps)
-    and no full block (M = 200)."""
-    out = []
-    for db in ('1', '0'):
-        monkeypatch.setenv('MAS_POL_ACT_DB', db)
-        p = _policy(D, seed=D + 5)
-        fp = FusedPolicy(p, D, torch.device('cuda'))
-        fp.pack()
-        g = torch.Generator(device='cuda').manual_seed(7)
-        obs = torch.randn((M, D), device='cuda', generator=g) * 2.0
-        xb = fp.x_buffer(M)
-        acts = torch.empty((M, 6), dtype=torch.int8, device='cuda')
-        lp = torch.empty((M,), device='cuda')
-        v = torch.empty((M,), device='cuda')
-        fp.act(obs, 3, 4, acts, lp, v, xb=xb, first_row=1000)
-        torch.cuda.synchronize()
-        out.append((acts, lp, v, xb))
-    for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
