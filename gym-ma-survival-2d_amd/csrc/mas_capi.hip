@@ -70,6 +70,8 @@ hipError_t policy_dw(int F, int G, int64_t K, const void* A, int64_t lda, const 
 namespace {
 
 constexpr int kWG = 64;  // threads per workgroup of k_step / k_reset (mas_step.h)
+// mas_step's default use of the side streams (MAS_SPLIT, mas_handle::split)
+constexpr int kSplitDefault = 2;
 
 thread_local std::string g_err;
 
@@ -318,8 +320,8 @@ struct mas_handle {
     // the slow split (launch_step): side stream + fork / join events, made at
     // the first mas_step that splits, on the handle's device.  split: 0 the
     // one-stream order, 2 (default) the slow list on the side stream;
-    // MAS_SPLIT=0/2 in the environment at mas_create, or
-    // mas_debug_force_general bit 3 (one stream)
+    // MAS_SPLIT=0/2 in the environment at mas_create (any other value is
+    // refused), or mas_debug_force_general bit 3 (one stream)
     StepSplit sp;
     bool sp_made;
     int split, split_default;
@@ -506,6 +508,15 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
         return fail(MAS_ERR_INVALID_ARG, "mas_create: unsupported safe-zone phases");
     if (c.lidar_n_lasers != 0 && (c.lidar_n_lasers < 2 || c.lidar_n_lasers > MAS_MAX_LASERS))
         return fail(MAS_ERR_INVALID_ARG, "mas_create: lidar n_lasers must be 0 or in [2, MAS_MAX_LASERS]");
+    // MAS_SPLIT: how mas_step uses the side streams (mas_handle::split)
+    int split_mode = kSplitDefault;
+    if (const char* v = getenv("MAS_SPLIT"); v && v[0]) {
+        if (!strcmp(v, "0")) split_mode = 0;
+        else if (!strcmp(v, "2")) split_mode = 2;
+        else
+            return fail(MAS_ERR_INVALID_ARG, "mas_create: MAS_SPLIT must be 0 (one stream) or 2 (the slow split); "
+                                             "modes 1 and 3 were removed");
+    }
     mas_handle* h = new (std::nothrow) mas_handle();
     if (!h) return fail(MAS_ERR_OOM, "mas_create: out of host memory");
     h->cfg = c;
@@ -566,8 +577,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->par = 0;
     h->sp_made = false;
     {
-        const char* v = getenv("MAS_SPLIT");
-        h->split = h->split_default = (v && v[0] == '0') ? 0 : 2;
+        h->split = h->split_default = split_mode;
         const char* k = getenv("MAS_SLOW_K");
         h->P.slow_k = k ? atoi(k) : 4;  // TOI events of an env's step that make it slow (the cap always does)
     }
@@ -701,17 +711,24 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
         h->sp_made = true;
     }
     // The general-path list's count is zeroed on the device after its last
-    // reader (launch_step), so the one-stream step (MAS_SPLIT=0) can be
-    // graph-captured and replayed.  The slow list's two count slots alternate
-    // per step (this step appends to one, its k_pre zeroes the other); the
-    // slow split itself is a host decision per step, so it is never captured.
+    // reader (launch_step), so a one-stream step can be graph-captured and
+    // replayed.  The slow list's two count slots alternate per step (this
+    // step appends to one, its k_pre zeroes the other) and the slow split is a
+    // host decision per step: neither may be captured, so while the caller's
+    // stream is capturing (hipStreamIsCapturing) the step runs on one stream.
     Params P = h->P;
     if (h->par) std::swap(P.slow_count, P.slow_prev);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing((hipStream_t)stream, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    // a captured step appends nothing to the slow list (slow_route 0): its
+    // k_pre zeroes the slot mas_debug_counters reads after it, on every replay
+    if (capturing) P.slow_prev = P.slow_count;
     // the slow split runs while the general kernels keep flagging slow envs
     // (the signal lags the device by the steps in flight: slow envs persist
-    // for many steps); without any, one stream and no fork / join
+    // for many steps); without any, no slow chain
     const StepSplit* sp = nullptr;
-    if (h->split == 2) {
+    if (h->split == 2 && !capturing) {
         if (__atomic_load_n(h->slow_sig, __ATOMIC_RELAXED)) {
             __atomic_store_n(h->slow_sig, 0, __ATOMIC_RELAXED);
             h->slow_hold = 8;
@@ -720,9 +737,8 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
             --h->slow_hold;
             sp = &h->sp;
         }
-    } else {
-        P.slow_k = 0;  // no slow flags, no signal
     }
+    if (h->split != 2) P.slow_k = 0;  // no slow flags, no signal
     h->ops.step(g, (hipStream_t)stream, P, h->state, h->N, actions, obs, rewards, done, auto_reset, sp);
     HIP_TRY(hipGetLastError());
     h->par ^= 1;

@@ -95,6 +95,7 @@ struct Params {
     int* list_overflow;  // appends to phys_list / slow_list / reset_list refused by their bounds (mas_debug_guards)
     int* reset_list;     // [N] the done envs of this step's post kernel (auto-reset; the side stream: its own list)
     int* reset_count;    // their count: zeroed by k_pre, appended by k_post_lanes, read by the reset launch
+    int reset_in_post;   // the auto-reset runs inside k_post_lanes (no reset list, no reset launch)
     int force_general;   // test diagnostics (mas_debug_force_general): every env takes the general physics path
     int solve_one_lane;  // A/B builds only (MAS_AB_KERNELS): the one-lane k_gen_solve + k_gen_toi
     uint8_t* gen_flag;  // [N] 1 = env e left the fast path this step (2: on the slow list)

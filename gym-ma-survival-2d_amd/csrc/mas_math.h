@@ -44,12 +44,28 @@ MAS_HD int opq(int x) { asm volatile("" : "+v"(x)); return x; }
 MAS_HD uint32_t opq(uint32_t x) { asm volatile("" : "+v"(x)); return x; }
 MAS_HD double opq(double x) { asm volatile("" : "+v"(x)); return x; }
 MAS_HD uint64_t opq(uint64_t x) { asm volatile("" : "+v"(x)); return x; }
+// a wave-uniform value (SGPRs) the compiler cannot see through: addresses
+// derived from it are not merged (CSE'd) with the kernel's other state
+// addresses, whose live ranges would otherwise span the kernel and spill
+MAS_HD int64_t opq_s(int64_t x) { asm volatile("" : "+s"(x)); return x; }
+template <class T>
+MAS_HD T* opq_s(T* p)
+{
+    asm volatile("" : "+s"(p));
+    return p;
+}
 #else
 MAS_HD float opq(float x) { return x; }
 MAS_HD int opq(int x) { return x; }
 MAS_HD uint32_t opq(uint32_t x) { return x; }
 MAS_HD double opq(double x) { return x; }
 MAS_HD uint64_t opq(uint64_t x) { return x; }
+MAS_HD int64_t opq_s(int64_t x) { return x; }
+template <class T>
+MAS_HD T* opq_s(T* p)
+{
+    return p;
+}
 #endif
 MAS_HD V2 opq(V2 v) { return mk(opq(v.x), opq(v.y)); }
 MAS_HD V2 add(V2 a, V2 b) { return mk(a.x + b.x, a.y + b.y); }

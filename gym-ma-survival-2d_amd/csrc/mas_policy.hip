@@ -1141,8 +1141,9 @@ static_assert(kLdsFrag % kDCopy == 0 && (kBk0 * 64) % kDCopy == 0 && (kBk1 * 64)
 // every store before them included) at the phase's first LDS read -- the
 // serialisation this kernel removes.  Invisible to that pass, the copies are
 // ordered only by land_db's explicit counts; the pass's own waits for other
-// loads can only over-wait (it does not count these).  m0 is set before every
-// copy: no other m0 user runs in this kernel.
+// loads can only over-wait (it does not count these).  The LDS base goes in
+// as an m0 operand ("{m0}"): the compiler sets m0 itself and knows it is
+// used (a clobber of the reserved m0 is not honoured).
 __device__ __forceinline__ void copy_db(bf8* __restrict__ buf, const bf8* __restrict__ src, int n)
 {
     const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
@@ -1152,7 +1153,7 @@ __device__ __forceinline__ void copy_db(bf8* __restrict__ buf, const bf8* __rest
     for (int k = 0; k < n; k += kDCopy) {
         const uint32_t m0v = lds0 + (uint32_t)k * 16u;
         const uint8_t* gk = g0 + (int64_t)k * 16;
-        asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0v), "v"(loff), "s"(gk) : "memory");
+        asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(loff), "s"(gk), "{m0}"(m0v) : "memory");
     }
 }
 // the stage copied one phase ago has landed in every wave: NST = this wave's
@@ -1297,7 +1298,11 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
         // (in-out operands: nothing derived from them is computed before)
         asm volatile("" : "+v"(aw0), "+v"(aw1), "+v"(adv), "+v"(old_lp), "+v"(ret)::"memory");
         // ---- E: W3^T; the loss gradient, dA2
-        land_db<38>();  // phase D: 6 loss-input loads + 32 h2 stores after them
+        // phase D: the 32 h2 stores after them (plus the loss-input loads, not
+        // counted: the compiler may combine the six 2-B / 4-B loads into fewer
+        // instructions, and a count above the real one would stop waiting too
+        // early; counting fewer only over-waits)
+        land_db<32>();
         const bf8* wb = buf(sc);
         copy_db(buf(sc + 1), F + Lo.wbk() + kBk0 * 64, kBk1 * 64);
 #pragma unroll

@@ -724,11 +724,225 @@ __device__ __forceinline__ void write_obs_row_seq(const PostV<C>& V, const Param
     o.finish();
 }
 
+// Cameras._update_seen (simulation.py:336-354) on agent lanes: camera i of
+// slot j.  slot_on: slot j takes part (its leader zeroes its seen rows and
+// records the alive mask the rays see); cam_on: this lane's agent is a live
+// camera of such a slot, at pos / angle ang; alive_m: the slot's alive mask.
+// Every candidate of the cone test goes into one wave-wide list, and the line
+// of sight rays are dealt over the 64 lanes (update_seen_dealt, mas_step.h:
+// the same candidates, rays and first-hit test).  Every lane calls it.
+template <class C>
+__device__ __forceinline__ void cameras_v(PostLds<C>& lds, const PostV<C>& V, const Params& P, bool slot_on,
+                                          bool cam_on, uint32_t alive_m, V2 pos, float ang, int i, int j, int lane)
+{
+    using PV = PostV<C>;
+    constexpr int S = kWG / C::AM, AM = C::AM;
+    if (i == 0 && slot_on) {
+        lds.alivem[j] = alive_m;
+#pragma unroll
+        for (int k = 0; k < C::NB; ++k) V.sn(k) = 0u;
+    }
+    uint64_t cand = 0;  // bit per body in the cone
+    int p = 0;
+    if (cam_on) {
+        p = __popc(alive_m & ((1u << i) - 1u));
+        const Rot q = rot_of(ang);
+        const int nb = V.nbox(), ni = V.nbi(), nh = V.nheal();
+#pragma unroll
+        for (int b = 0; b < C::BM; ++b) {
+            if (b < nb && poly_test_point(P.cone, pos, q, V.bp(b))) cand |= 1ull << (BIdx<C>::box + b);
+            if (b < ni && poly_test_point(P.cone, pos, q, V.ip(b))) cand |= 1ull << (BIdx<C>::bitem + b);
+        }
+#pragma unroll
+        for (int h = 0; h < C::HM; ++h)
+            if (h < nh && poly_test_point(P.cone, pos, q, V.hp(h))) cand |= 1ull << (BIdx<C>::heal + h);
+#pragma unroll
+        for (int w = 0; w < kNumWalls; ++w)
+            if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) cand |= 1ull << (BIdx<C>::wall + w);
+#pragma unroll
+        for (int k = 0; k < AM; ++k)
+            if (k != i && bit(alive_m, k) && poly_test_point(P.cone, pos, q, V.agent(k)))
+                cand |= 1ull << (BIdx<C>::agent + k);
+    }
+    // the wave's rays dealt over its lanes (update_seen_cam)
+    const int np = __popcll(cand);
+    int incl = np;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int total = __shfl(incl, 63, 64);
+    int at = incl - np;
+    while (cand) {
+        const int body = __builtin_ctzll(cand);
+        cand &= cand - 1;
+        lds.u.cam.list[at++] = (uint16_t)((p << 12) | (lane << 6) | body);
+    }
+    wave_lds_sync();  // the list, the agent table and the zeroed seen rows are visible
+    const float eps1 = (float)(1.0 + 1e-6);
+    for (int t = lane; t < total; t += 64) {
+        const uint32_t en = lds.u.cam.list[t];
+        const int body = (int)(en & 63u), o = (int)((en >> 6) & 63u), pc = (int)(en >> 12);
+        const int so = o / AM, co = o - so * AM;  // the owner's slot and camera
+        const PV Vo{&lds, so};
+        const V2 opos = Vo.agent(co);
+        V2 oc;
+        if (body < BIdx<C>::bitem) oc = Vo.bp(body);
+        else if (body < BIdx<C>::heal) oc = Vo.ip(body - BIdx<C>::bitem);
+        else if (body < BIdx<C>::wall) oc = Vo.hp(body - BIdx<C>::heal);
+        else if (body < BIdx<C>::agent) {
+            const int w = body - BIdx<C>::wall;
+            oc = opq(P.wall_pos[0]);
+#pragma unroll
+            for (int q2 = 1; q2 < kNumWalls; ++q2)
+                if (q2 == w) oc = opq(P.wall_pos[q2]);
+        } else oc = Vo.agent(body - BIdx<C>::agent);
+        const V2 d = sub(oc, opos);
+        const V2 end = add(opos, scl(eps1, d));
+        if (ray_cast_pv(P, Vo, lds.alivem[so], opos, end) == body) atomicOr(&lds.seen[body * S + so], 1u << pc);
+    }
+    wave_lds_sync();  // the seen rows are complete
+}
+
+// BaseEnv.reset -> Simulation.reset (masurvival_env.py:59-74; env_reset,
+// mas_step.h, the same draws in the same order) of slot j on its leader lane,
+// into the slot's LDS groups: SpawnGrid.reset's shuffle of the grid cells
+// (semantics.py:71-74, 987-992), RandomizeBoxShapes (:107-120) and the
+// spawns (boxes, heals, agents from the end of the permutation), empty box
+// items, the SafeZone's post_reset (:739-756).  The agent table gets the
+// agents' spawn poses and full health.  R: the env's PCG64 stream; perm: the
+// [grid cells][S] byte scratch.  Fisher-Yates from the top finalises cell i
+// at step i and later steps touch only lower cells, so the swaps run only
+// for the cells the spawns take (the draws of every step are still made).
+template <class C>
+__device__ __forceinline__ void reset_env_v(const PostV<C>& V, const Params& P, EnvL<C>& R, uint8_t* perm)
+{
+    using PV = PostV<C>;
+    constexpr int S = PV::S;
+    const int A = P.A, H = P.H, B = P.B;
+    const int g = P.grid_size, n = g * g;
+    auto pm = [&](int k) -> uint8_t& { return perm[k * S + V.j]; };
+    const int used = A + H + B;  // <= n (mas_create)
+    for (int k = 0; k < n; ++k) pm(k) = (uint8_t)k;
+    for (int i = n - 1; i >= 1; --i) {
+        const int jj = (int)pcg_interval32(R, (uint32_t)i);
+        if (i >= n - used) {
+            const uint8_t t = pm(i);
+            pm(i) = pm(jj);
+            pm(jj) = t;
+        }
+    }
+    int top = n;
+    auto cell = [&](int k) -> V2 {
+        const int ii = k % g, jj = k / g;
+        double ci = (double)ii / g + 0.5 / g;
+        double cj = (double)jj / g + 0.5 / g;
+        ci = P.floor_size * ci - P.floor_size / 2.0;
+        cj = P.floor_size * cj - P.floor_size / 2.0;
+        return mk((float)ci, (float)cj);
+    };
+    // boxes: sizes (RandomizeBoxShapes draws), then the spawn cells
+    V.bw(0) = (uint32_t)B;  // (<= C::BM, mas_create)
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        float hx = 0.0f, hy = 0.0f;
+        if (b < B) {
+            hx = P.box_hx;
+            hy = P.box_hy;
+            if (P.randomized) {
+                double wv = P.avg_w + P.std_w * pcg_normal(R);
+                wv = P.min_w > wv ? P.min_w : wv;
+                double hv = P.avg_h + P.std_h * pcg_normal(R);
+                hv = P.min_h > hv ? P.min_h : hv;
+                hx = (float)(wv / 2.0);
+                hy = (float)(hv / 2.0);
+            }
+        }
+        V.bw(3 + 6 * b) = __float_as_uint(hx);
+        V.bw(4 + 6 * b) = __float_as_uint(hy);
+    }
+#pragma unroll
+    for (int b = 0; b < C::BM; ++b) {
+        const V2 c = b < B ? cell(pm(--top)) : mk(0.0f, 0.0f);
+        V.bw(1 + 6 * b) = __float_as_uint(c.x);
+        V.bw(2 + 6 * b) = __float_as_uint(c.y);
+        V.bw(5 + 6 * b) = (uint32_t)mk_boxmeta(0, 0, b < B ? 1 : 0, kCauseNone, kCauseNone);
+        V.bw(6 + 6 * b) = (uint32_t)(b < B ? P.box_health : 0);
+    }
+    // box items: none
+    V.iw(0) = 0u;
+#pragma unroll
+    for (int q = 1; q < Lay<C>::kItemW; ++q) V.iw(q) = 0u;
+    // heals
+    V.hw(0) = (uint32_t)H;
+#pragma unroll
+    for (int h = 0; h < C::HM; ++h) {
+        const V2 c = h < H ? cell(pm(--top)) : mk(0.0f, 0.0f);
+        V.hw(1 + 2 * h) = __float_as_uint(c.x);
+        V.hw(2 + 2 * h) = __float_as_uint(c.y);
+    }
+    // agents: the agent table (pose, velocity 0, health)
+#pragma unroll
+    for (int k = 0; k < C::AM; ++k) {
+        const V2 c = k < A ? cell(pm(--top)) : mk(0.0f, 0.0f);
+        V.ag(0, k) = c.x;
+        V.ag(1, k) = c.y;
+#pragma unroll
+        for (int f = 2; f < 6; ++f) V.ag(f, k) = 0.0f;
+        V.ag(6, k) = k < A ? (float)P.agent_health : 0.0f;
+    }
+    // SafeZone.post_reset
+    V2 zc[kMaxPhases];
+#pragma unroll
+    for (int k = 0; k < kMaxPhases; ++k) zc[k] = mk(0.0f, 0.0f);
+    const int nr = P.zone_nr;
+    if (P.zone_random) {
+        for (int k = nr; k >= 0; --k) {
+            double r = 0.0;
+#pragma unroll
+            for (int q = 0; q < kMaxPhases; ++q)
+                if (q == k) r = opq(P.zrad[q]);
+            const double Lz = P.floor_size - 2.0 * r;
+            const double cx = (pcg_random(R) * Lz) - Lz / 2.0;
+            const double cy = (pcg_random(R) * Lz) - Lz / 2.0;
+            put(zc, k, mk((float)cx, (float)cy));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMaxPhases; ++k)
+            if (k < nr) zc[k] = mk(P.zfix[k][0], P.zfix[k][1]);
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxPhases; ++k) {
+        V.zw(2 * k) = __float_as_uint(zc[k].x);
+        V.zw(2 * k + 1) = __float_as_uint(zc[k].y);
+    }
+    V.zw(PV::kZPhase) = 0u;
+    V.zw(PV::kZCd) = (uint32_t)P.zone_cooldown;
+    V.zw(PV::kZSh) = 0u;
+    V.zw(PV::kZEnd) = 0u;
+    V.zw(PV::kZPx) = __float_as_uint(zc[0].x);
+    V.zw(PV::kZPy) = __float_as_uint(zc[0].y);
+    V.zw(PV::kZRad) = __float_as_uint(P.zradf[0]);
+}
+
+// The auto-reset runs inside k_post_lanes (reset_in_post) when the spawn
+// grid's permutation scratch fits the LDS union of its slots
+template <class C>
+constexpr int kPostUnionBytes = (int)sizeof(((PostLds<C>*)nullptr)->u);
+template <class C>
+inline bool reset_fits_post(const Params& P)
+{
+    return P.grid_size * P.grid_size * (kWG / C::AM) <= kPostUnionBytes<C>;
+}
+
 // The post-physics phases of one step on agent lanes (see the file comment),
 // over env selection M (kAllEnvs / kMainEnvs on the caller's stream, the
-// slow list's kGenEnvs on the side stream).  Done envs are appended to the
-// selection's reset list (auto-reset: the k_obs reset launch over that list
-// follows, launch_post).
+// slow list's kGenEnvs on the side stream).  With the auto-reset (ar) the
+// done envs are reset in place at the end (P.reset_in_post: their state and
+// obs rows are the reset env's), or appended to the selection's reset list
+// for the k_obs reset launch over that list (launch_post).
 // waves per SIMD the register budget targets (3: <= 168 VGPRs)
 #ifndef MAS_POST_OCC
 #define MAS_POST_OCC 3
@@ -840,75 +1054,7 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
         }
     }
     // ---- Cameras.post_step (simulation.py:314-354): camera i of slot j
-    {
-        if (i == 0) {
-            lds.alivem[j] = alive_m;
-#pragma unroll
-            for (int k = 0; k < C::NB; ++k) V.sn(k) = 0u;
-        }
-        uint64_t cand = 0;  // bit per body in the cone
-        int p = 0;
-        if (valid && alive) {
-            p = __popc(alive_m & ((1u << i) - 1u));
-            const V2 pos = g.c;
-            const Rot q = rot_of(g.a);
-            const int nb = V.nbox(), ni = V.nbi(), nh = V.nheal();
-#pragma unroll
-            for (int b = 0; b < C::BM; ++b) {
-                if (b < nb && poly_test_point(P.cone, pos, q, V.bp(b))) cand |= 1ull << (BIdx<C>::box + b);
-                if (b < ni && poly_test_point(P.cone, pos, q, V.ip(b))) cand |= 1ull << (BIdx<C>::bitem + b);
-            }
-#pragma unroll
-            for (int h = 0; h < C::HM; ++h)
-                if (h < nh && poly_test_point(P.cone, pos, q, V.hp(h))) cand |= 1ull << (BIdx<C>::heal + h);
-#pragma unroll
-            for (int w = 0; w < kNumWalls; ++w)
-                if (poly_test_point(P.cone, pos, q, P.wall_pos[w])) cand |= 1ull << (BIdx<C>::wall + w);
-#pragma unroll
-            for (int k = 0; k < AM; ++k)
-                if (k != i && bit(alive_m, k) && poly_test_point(P.cone, pos, q, V.agent(k)))
-                    cand |= 1ull << (BIdx<C>::agent + k);
-        }
-        // the wave's rays dealt over its lanes (update_seen_cam)
-        const int np = __popcll(cand);
-        int incl = np;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        const int total = __shfl(incl, 63, 64);
-        int at = incl - np;
-        while (cand) {
-            const int body = __builtin_ctzll(cand);
-            cand &= cand - 1;
-            lds.u.cam.list[at++] = (uint16_t)((p << 12) | (lane << 6) | body);
-        }
-        wave_lds_sync();  // the list, the fixture tables and the zeroed seen rows are visible
-        const float eps1 = (float)(1.0 + 1e-6);
-        for (int t = lane; t < total; t += 64) {
-            const uint32_t en = lds.u.cam.list[t];
-            const int body = (int)(en & 63u), o = (int)((en >> 6) & 63u), pc = (int)(en >> 12);
-            const int so = o / AM, co = o - so * AM;  // the owner's slot and camera
-            const PV Vo{&lds, so};
-            const V2 opos = Vo.agent(co);
-            V2 oc;
-            if (body < BIdx<C>::bitem) oc = Vo.bp(body);
-            else if (body < BIdx<C>::heal) oc = Vo.ip(body - BIdx<C>::bitem);
-            else if (body < BIdx<C>::wall) oc = Vo.hp(body - BIdx<C>::heal);
-            else if (body < BIdx<C>::agent) {
-                const int w = body - BIdx<C>::wall;
-                oc = opq(P.wall_pos[0]);
-#pragma unroll
-                for (int q2 = 1; q2 < kNumWalls; ++q2)
-                    if (q2 == w) oc = opq(P.wall_pos[q2]);
-            } else oc = Vo.agent(body - BIdx<C>::agent);
-            const V2 d = sub(oc, opos);
-            const V2 end = add(opos, scl(eps1, d));
-            if (ray_cast_pv(P, Vo, lds.alivem[so], opos, end) == body) atomicOr(&lds.seen[body * S + so], 1u << pc);
-        }
-        wave_lds_sync();  // the seen rows are complete
-    }
+    cameras_v<C>(lds, V, P, true, valid && alive, alive_m, g.c, g.a, i, j, lane);
     MAS_PROF(P, 42);
     // ---------------- agents post_step (step_post, mas_step.h) ----------------
     uint32_t dirty = kGZone | kGStat;
@@ -1184,11 +1330,15 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
         }
     }
     MAS_PROF(P, 43);
+    // the auto-reset in place (reset_in_post): a done env's post-step groups
+    // are not stored, its reset state is (below)
+    const bool rs = ar && P.reset_in_post && valid && is_done;
+    const bool st_ok = valid && !rs;
     // ---------------- stores: the groups this step changed ----------------
     uint32_t dirty_env = dirty;
 #pragma unroll
     for (int o = 1; o < AM; o <<= 1) dirty_env |= (uint32_t)__shfl_xor((int)dirty_env, o, 64);
-    if (valid) {
+    if (st_ok) {
         if (dirty_env & kGRule) {
             const int wr = LY::rule + i * LY::kRuleA;
             state[state_index(wr, e, N)] = (uint32_t)g.health;
@@ -1219,17 +1369,100 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
         }
     }
     {
-        const uint32_t sv = slot_mask<C>(valid);
-        const uint32_t sb = slot_mask<C>(valid && bchanged);
-        const uint32_t si = slot_mask<C>(valid && (dirty_env & kGItem));
-        const uint32_t sh = slot_mask<C>(valid && (dirty_env & kGHeal));
+        const uint32_t sv = slot_mask<C>(st_ok);
+        const uint32_t sb = slot_mask<C>(st_ok && bchanged);
+        const uint32_t si = slot_mask<C>(st_ok && (dirty_env & kGItem));
+        const uint32_t sh = slot_mask<C>(st_ok && (dirty_env & kGHeal));
         if (sb) slot_store<S, LY::kBoxW>(lds.box, state, N, lds.eidx, LY::box, sb);
         if (si) slot_store<S, LY::kItemW>(lds.item, state, N, lds.eidx, LY::item, si);
         if (sh) slot_store<S, LY::kHealW>(lds.heal, state, N, lds.eidx, LY::heal, sh);
         if (sv) slot_store<S, LY::kZoneW>(lds.zone, state, N, lds.eidx, LY::zone, sv);
     }
-    // ---------------- auto-reset list: the done envs ----------------
-    if (ar) {
+    // ---------------- auto-reset: the done envs ----------------
+    if (ar && P.reset_in_post) {
+        if (__any(rs)) {
+            // BaseEnv.reset (masurvival_env.py:59-74) of the done envs in
+            // place: the same state and obs rows as env_reset + update_seen
+            // of the reset launch (k_obs), with the groups built in this
+            // kernel's LDS.  The reset overwrites words this kernel stored for
+            // the env from other lanes (DeathDrop, the contact rows): those
+            // stores complete first (vmcnt counts stores on gfx9)
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            // (this block's state addresses from an opaque base: merged with
+            // the kernel's other addresses they stayed live across it and spilled)
+            uint32_t* const stR = opq_s(state);
+            const int64_t NR = opq_s(N);
+            if (rs && i == 0) {
+                EnvL<C> R;
+                Loader ld{stR, NR, e, 0};
+                visit_state(R, ld, kGRng);  // (after the DeathDrop draws above)
+                reset_env_v<C>(V, P, R, reinterpret_cast<uint8_t*>(&lds.u));
+                Storer sr{stR, NR, e, 0};
+                visit_state(R, sr, kGRng);
+                P.slow_flag[e] = 0;  // a new episode: no slow-list history
+            }
+            wave_lds_sync();  // the reset groups and agent table are in LDS
+            const uint32_t am_reset = (A >= 32) ? 0xffffffffu : ((1u << A) - 1u);
+            if (rs) {
+                // this lane's agent: its spawn pose, at rest, full health, empty inventory
+                g.c = V.agent(i);
+                g.a = 0.0f;
+                g.v = mk(0.0f, 0.0f);
+                g.w = 0.0f;
+                g.sleep = 0.0f;
+                g.health = i < A ? P.agent_health : 0;
+                g.cause = kCauseNone;
+                g.cooldown = 0;
+                g.inv_n = 0;
+#pragma unroll
+                for (int k = 0; k < C::SM; ++k) {
+                    g.inv_meta[k] = 0;
+                    g.inv_hx[k] = 0.0f;
+                    g.inv_hy[k] = 0.0f;
+                }
+                alive_m = am_reset;
+                awake_m = am_reset;
+                alive = i < A;
+            }
+            // Cameras.post_reset: the reset envs' cameras only
+            cameras_v<C>(lds, V, P, rs, rs && alive, alive_m, g.c, g.a, i, j, lane);
+            // every group but the stats (visit_state order, kResetSt)
+            if (rs) {
+                const float d[7] = {g.c.x, g.c.y, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int q = 0; q < 7; ++q) stR[state_index(7 * i + q, e, NR)] = __float_as_uint(d[q]);
+                const int wr = LY::rule + i * LY::kRuleA;
+                stR[state_index(wr, e, NR)] = (uint32_t)g.health;
+                stR[state_index(wr + 1, e, NR)] = (uint32_t)g.cause;
+                stR[state_index(wr + 2, e, NR)] = 0u;
+                stR[state_index(wr + 3, e, NR)] = 0u;
+#pragma unroll
+                for (int k = 0; k < 3 * C::SM; ++k) stR[state_index(wr + 4 + k, e, NR)] = 0u;
+                // the contact memory (a new b2World), dealt over the env's lanes
+                for (int k = i; k < Cont<C>::kWords; k += AM) stR[state_index(P.w_cont + k, e, NR)] = 0u;
+                if (i == 0) {
+                    stR[state_index(LY::alive, e, NR)] = am_reset;
+                    stR[state_index(LY::awake, e, NR)] = am_reset;
+                    stR[state_index(LY::invdt, e, NR)] = 0u;
+#pragma unroll
+                    for (int q = 0; q < LY::kItemW; ++q) stR[state_index(LY::pend + q, e, NR)] = 0u;
+#pragma unroll
+                    for (int w = 0; w < kSeenWords<C>; ++w) {
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (4 * w + q < C::NB) x |= (V.sn(4 * w + q) & 0xffu) << (8 * q);
+                        stR[state_index(LY::seen + w, e, NR)] = x;
+                    }
+                }
+            }
+            const uint32_t sr = slot_mask<C>(rs);
+            slot_store<S, LY::kBoxW>(lds.box, stR, NR, lds.eidx, LY::box, sr);
+            slot_store<S, LY::kItemW>(lds.item, stR, NR, lds.eidx, LY::item, sr);
+            slot_store<S, LY::kHealW>(lds.heal, stR, NR, lds.eidx, LY::heal, sr);
+            slot_store<S, LY::kZoneW>(lds.zone, stR, NR, lds.eidx, LY::zone, sr);
+        }
+    } else if (ar) {
         const bool mine = valid && i == 0 && is_done;
         const uint64_t m = __ballot(mine);
         if (m) {

@@ -1,6 +1,8 @@
 #!/bin/bash
 # One GPU measurement pass (run via gpurun from the repo root):
-#   scripts/gpu_round.sh <tag> [tests] [smoke] [bench] [prof] [pmc] [env] [envprof]
+#   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
+#   tests t:<files> ab smoke bench env full profd envprof pmc pmcenv profgen
+#   proflanes splitab libab:<variant>)
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
 R=$GRAFT_REPO_ROOT
@@ -71,6 +73,42 @@ for step in "$@"; do
     profgen)
       cd $R && timeout -k 10 300 python -u profiles/prof_toi.py 65536 4 > $O/prof_toi.log 2>&1 || exit $?
       cd $R && timeout -k 10 300 python -u profiles/prof_general.py 65536 20 --ppo > $O/prof_general.log 2>&1 || exit $? ;;
+    splitab)
+      # MAS_SPLIT A/B (same box, alternating processes): driver window and env-only 2v2 / FFA4
+      for sp in 2 3 2 3; do
+        cd $R && MAS_SPLIT=$sp timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/splitab_driver_sp$sp.json 2>> $O/splitab.err || exit 1
+      done
+      for sp in 2 3 2 3; do
+        cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline >> $O/splitab_env_sp$sp.json 2>> $O/splitab.err || exit 1
+        cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline >> $O/splitab_ffa_sp$sp.json 2>> $O/splitab.err || exit 1
+      done ;;
+    libab:*)
+      # libab:<variant>: driver window + env-only 2v2, default library vs masurvival/_lib/libmas_<variant>.so, alternating
+      V=${step#libab:}
+      for k in 1 2; do
+        for lib in default $V; do
+          L=""; [ $lib != default ] && L="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$lib.so"
+          cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $L >> $O/libab_driver_$lib.json 2>> $O/libab.err || exit 1
+          cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline $L >> $O/libab_env_$lib.json 2>> $O/libab.err || exit 1
+        done
+      done ;;
+    pmcenv)
+      # FETCH_SIZE / WRITE_SIZE passes of the env-only workloads (2v2, FFA4 shard, 1v1, C4 / C5 full)
+      for cfg in "2v2 65536 40 10" "ffa4 16384 40 10" "1v1 4096 60 10" "2v2 262144 20 10" "ffa4 131072 15 10"; do
+        set -- $cfg
+        for c in FETCH_SIZE WRITE_SIZE; do
+          cd /tmp && timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "mas::k_" --output-format csv \
+            -d $O/pmc_${c}_$1_$2 -o run -- python3 $R/bench.py --mode env --config $1 --envs $2 --steps $3 --warmup $4 --no-cpu-baseline > $O/pmc_${c}_$1_$2.log 2>&1 || exit 1
+        done
+      done ;;
+    profsplit)
+      # kernel traces of the driver window under MAS_SPLIT 2 and 3 (profiles/timeline.py)
+      for sp in 2 3; do
+        cd /tmp && MAS_SPLIT=$sp timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sp$sp -o run -- \
+          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_sp$sp.log 2>&1 || exit $?
+      done ;;
+    proflanes)
+      cd $R && timeout -k 10 200 python -u profiles/prof_lanes.py 2v2 65536 20 > $O/prof_lanes_2v2.txt 2>&1 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"

@@ -42,3 +42,17 @@ def test_create_rejects_bad_config_without_gpu():
     rc = lib.mas_create(ctypes.byref(cfg), 4, 0, ctypes.byref(h))
     assert rc == -1
     assert b'n_agents' in lib.mas_last_error()
+
+
+@pytest.mark.parametrize('val', ['1', '3', 'x'])
+def test_create_rejects_unknown_split_mode_without_gpu(val, monkeypatch):
+    """MAS_SPLIT takes 0 (one stream) or 2 (the slow split); the removed modes
+    and anything else are refused before any device allocation."""
+    monkeypatch.setenv('MAS_SPLIT', val)
+    lib = abi.load_library()
+    from masurvival.config import ResolvedConfig
+    cfg = ResolvedConfig(None).to_struct()
+    h = ctypes.c_void_p()
+    rc = lib.mas_create(ctypes.byref(cfg), 4, 0, ctypes.byref(h))
+    assert rc == -1
+    assert b'MAS_SPLIT' in lib.mas_last_error()

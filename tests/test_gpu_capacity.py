@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 
 import golden_replay as gr  # noqa: E402
 from masurvival import abi  # noqa: E402
+from gpu_util import class_missing  # noqa: E402
 from masurvival.config import ResolvedConfig, pcg64_state  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 from oracle import OracleEnv  # noqa: E402
@@ -50,7 +51,7 @@ def test_large_capacity_configs_match_oracle(name, cfg, n, T):
     try:
         env = VecMaSurvival(cfg, n_envs=n, seeds=range(500, 500 + n), auto_reset=True)
     except abi.MasError as e:
-        pytest.skip(str(e))
+        class_missing(e)
     ors = [OracleEnv(rc.to_struct(), pcg64_state(500 + e)) for e in range(n)]
     obs = env.reset().cpu().numpy()
     for e in range(n):

@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 
 import golden_replay as gr  # noqa: E402
 from masurvival import abi  # noqa: E402
+from gpu_util import class_missing  # noqa: E402
 from masurvival.config import C3_CONFIG, C5_CONFIG, ResolvedConfig, pcg64_state  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 from oracle import OracleEnv  # noqa: E402
@@ -36,9 +37,7 @@ def test_full_config_sampled_envs_match_oracle(name, cfg, n, T):
     try:
         env = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
     except abi.MasError as e:
-        if 'no compiled capacity class' in str(e):
-            pytest.skip(str(e))
-        raise
+        class_missing(e)
     sample = _sample(n, 24, n)
     ors = {e: OracleEnv(rc.to_struct(), pcg64_state(e)) for e in sample}
     obs = env.reset()

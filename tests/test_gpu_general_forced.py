@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 import golden_replay as gr  # noqa: E402
 from masurvival import abi  # noqa: E402
+from gpu_util import class_missing  # noqa: E402
 from masurvival.config import C3_CONFIG, C5_CONFIG, ResolvedConfig, pcg64_state  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 from oracle import OracleEnv  # noqa: E402
@@ -32,7 +33,7 @@ def test_all_envs_on_general_path_match_oracle(name, cfg, n, T):
     try:
         env = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
     except abi.MasError as e:
-        pytest.skip(str(e))
+        class_missing(e)
     env.force_general(True)
     s = {0, 1, 31, 32, 63, 64, n // 2, n - 33, n - 32, n - 2, n - 1}
     s |= set(np.random.default_rng(n).choice(n, size=24, replace=False).tolist())

@@ -8,13 +8,19 @@ handle steps eagerly, a second replays a HIP graph of one captured step with
 the same actions copied into its static action buffer; obs, rewards, done,
 the general-path counts and the final state images must be identical, and no
 list append may be refused (a count that grew across replays would re-step
-stale entries and then overflow the list)."""
+stale entries and then overflow the list).
+
+mas_step checks hipStreamIsCapturing: a step captured on a handle with the
+default slow split while it is on (MAS_SLOW_K=1 and a warm-up that flags
+slow envs, so the 8-step hold is active at capture) runs on one stream in
+the graph and replays like eager steps of a one-stream handle."""
 import pytest
 
 torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
 from masurvival import abi  # noqa: E402
+from gpu_util import class_missing  # noqa: E402
 from masurvival.config import C3_CONFIG, C5_CONFIG  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 
@@ -30,9 +36,7 @@ def test_captured_step_replays_like_eager(name, cfg, n, T, forced):
         eager = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
         graph = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
     except abi.MasError as e:
-        if 'no compiled capacity class' in str(e):
-            pytest.skip(str(e))
-        raise
+        class_missing(e)
     for e in (eager, graph):
         e.split_step(0)
         if forced:
@@ -55,6 +59,58 @@ def test_captured_step_replays_like_eager(name, cfg, n, T, forced):
         assert torch.equal(d1, graph.dones), (name, t)
         assert torch.equal(r1, graph.rewards), (name, t)
         assert torch.equal(o1, graph.obs), (name, t)
+        c1, c2 = eager.debug_counters()['phys_general_envs'], graph.debug_counters()['phys_general_envs']
+        assert c1 == c2, (name, t, c1, c2)
+        general += c1
+    assert general > 0
+    assert torch.equal(eager.get_state(), graph.get_state())
+    assert eager.debug_guards()['list_overflow'] == 0
+    assert graph.debug_guards()['list_overflow'] == 0
+    del g
+    eager.close()
+    graph.close()
+
+
+def test_captured_step_of_split_handle_replays_like_eager(monkeypatch):
+    name, mode = 'slow split held at capture', None
+    monkeypatch.setenv('MAS_SLOW_K', '1')
+    monkeypatch.delenv('MAS_SPLIT', raising=False)
+    n, T, warm = 4096, 100, 40
+    try:
+        eager = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n), auto_reset=True)
+        graph = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n), auto_reset=True)
+    except abi.MasError as e:
+        pytest.fail(str(e))
+    eager.split_step(0)
+    graph.split_step(mode)
+    assert torch.equal(eager.reset(), graph.reset())
+    gen = torch.Generator(device=graph.device)
+    gen.manual_seed(n + 29)
+    hi = HI.to(graph.device)
+    side = 0
+    for t in range(warm):
+        # eager warm-up on both: the graph handle's slow split turns on
+        a = (torch.rand((n, graph.n_agents, 6), generator=gen, device=graph.device) * hi).to(torch.int8)
+        o1, _, _, _ = eager.step(a)
+        o2, _, _, _ = graph.step(a)
+        assert torch.equal(o1, o2), (name, t)
+        side += int((graph.gen_flags() == 2).sum())
+    assert side > 0, name  # the slow list ran before the capture
+    act = torch.zeros((n, graph.n_agents, 6), dtype=torch.int8, device=graph.device)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        graph.step(act)
+    general = 0
+    for t in range(T):
+        a = (torch.rand((n, graph.n_agents, 6), generator=gen, device=graph.device) * hi).to(torch.int8)
+        act.copy_(a)
+        g.replay()
+        o1, r1, d1, _ = eager.step(a)
+        assert torch.equal(d1, graph.dones), (name, t)
+        assert torch.equal(r1, graph.rewards), (name, t)
+        assert torch.equal(o1, graph.obs), (name, t)
+        assert not bool((graph.gen_flags() == 2).any()), (name, t)  # no slow list in the graph
         c1, c2 = eager.debug_counters()['phys_general_envs'], graph.debug_counters()['phys_general_envs']
         assert c1 == c2, (name, t, c1, c2)
         general += c1

@@ -24,6 +24,7 @@ pytestmark = pytest.mark.gpu
 
 import golden_replay as gr  # noqa: E402
 from masurvival import abi  # noqa: E402
+from gpu_util import class_missing  # noqa: E402
 from masurvival.config import ResolvedConfig, pcg64_state  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 from oracle import OracleEnv  # noqa: E402
@@ -60,9 +61,7 @@ def _make(cfg, n):
     try:
         return VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
     except abi.MasError as e:
-        if 'no compiled capacity class' in str(e):
-            pytest.skip(str(e))
-        raise
+        class_missing(e)
 
 
 def _run(cfg, n, T, reset_every, seed):

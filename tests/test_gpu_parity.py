@@ -13,6 +13,7 @@ pytestmark = pytest.mark.gpu
 
 import golden_replay as gr  # noqa: E402
 from masurvival import abi  # noqa: E402
+from gpu_util import class_missing  # noqa: E402
 from masurvival.config import C3_CONFIG, C5_CONFIG, ResolvedConfig, pcg64_state  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 from oracle import OracleEnv  # noqa: E402
@@ -22,9 +23,7 @@ def make_vec(cfg, n, seeds, auto_reset):
     try:
         return VecMaSurvival(cfg, n_envs=n, seeds=seeds, auto_reset=auto_reset)
     except abi.MasError as e:
-        if 'no compiled capacity class' in str(e):
-            pytest.skip(str(e))
-        raise
+        class_missing(e)
 
 
 @pytest.mark.parametrize('name', gr.golden_files())

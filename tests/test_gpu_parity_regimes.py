@@ -24,6 +24,7 @@ pytestmark = pytest.mark.gpu
 import golden_replay as gr  # noqa: E402
 import oracle  # noqa: E402
 from masurvival import abi  # noqa: E402
+from gpu_util import class_missing  # noqa: E402
 from masurvival.config import C1_CONFIG, C3_CONFIG, C5_CONFIG, ResolvedConfig, pcg64_state  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 from oracle import OracleEnv  # noqa: E402
@@ -35,9 +36,7 @@ def make_vec(cfg, n, seeds, auto_reset=True):
     try:
         return VecMaSurvival(cfg, n_envs=n, seeds=seeds, auto_reset=auto_reset)
     except abi.MasError as e:
-        if 'no compiled capacity class' in str(e):
-            pytest.skip(str(e))
-        raise
+        class_missing(e)
 
 
 def _sample(n, k_random, seed):
@@ -213,7 +212,7 @@ def test_facade_dict_obs_match_golden(name):
     try:
         env = MaSurvival(cfg)
     except abi.MasError as e:
-        pytest.skip(str(e))
+        class_missing(e)
     env.np_random = np.random.default_rng(int(d['env_seed']))
     obs = env.reset()
     assert sorted(obs.keys()) == keys
