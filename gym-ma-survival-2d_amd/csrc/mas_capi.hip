@@ -313,7 +313,8 @@ struct mas_handle {
     int device;
     uint32_t* state;
     uint64_t* seedbuf;
-    int* phys;  // [N] env list + [1] count (k_pre -> general path) + [1] invalid-action count + [1] last count + [1] list guard
+    int* phys;  // the general-path list (k_pre -> general path, sharded) + [1] (unused) + [1] invalid-action count
+                // + [1] last count + [1] list guard, then the list's shard counts (Params::list_shards)
     uint8_t* gen_flag;  // [N] env left the fast path this step
     float* sweep;       // A/B builds only (MAS_AB_KERNELS): k_gen_solve -> k_gen_toi
     mas_obs_layout layout;
@@ -559,8 +560,13 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMalloc(&h->seedbuf, (size_t)n_envs * 6 * 8);
     h->P.prof = nullptr;
     h->phys = nullptr;
-    if (e == hipSuccess) e = hipMalloc(&h->phys, ((size_t)n_envs + 8) * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(h->phys, 0, ((size_t)n_envs + 8) * sizeof(int));
+    // [N + kListSlack] the general-path list (its shards), [8] counters, then
+    // the kListShards shard counts kShardStride ints apart (256-B aligned)
+    const size_t list_ints = (size_t)n_envs + kListSlack;
+    const size_t shard_at = (list_ints + 8 + kShardStride - 1) / kShardStride * kShardStride;
+    const size_t phys_ints = shard_at + (size_t)kListShards * kShardStride;
+    if (e == hipSuccess) e = hipMalloc(&h->phys, phys_ints * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(h->phys, 0, phys_ints * sizeof(int));
     h->sweep = nullptr;
 #if MAS_AB_KERNELS
     if (e == hipSuccess) e = hipMalloc(&h->sweep, (size_t)n_envs * 3 * kSweepAgents * sizeof(float));
@@ -571,9 +577,11 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     if (e == hipSuccess) e = hipMemset(h->gen_flag, 0, (size_t)n_envs);
     h->P.gen_flag = h->gen_flag;
     h->P.phys_list = h->phys;
-    h->P.phys_count = h->phys ? h->phys + n_envs : nullptr;
-    h->P.bad_actions = h->phys ? h->phys + n_envs + 1 : nullptr;
-    h->P.phys_last = h->phys ? h->phys + n_envs + 2 : nullptr;
+    h->P.phys_count = h->phys ? h->phys + shard_at : nullptr;
+    h->P.list_shards = 1;  // (launch_step sets the step's sharding)
+    h->P.list_cap = (int)n_envs;
+    h->P.bad_actions = h->phys ? h->phys + list_ints + 1 : nullptr;
+    h->P.phys_last = h->phys ? h->phys + list_ints + 2 : nullptr;
     h->par = 0;
     h->sp_made = false;
     {
@@ -581,7 +589,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
         const char* k = getenv("MAS_SLOW_K");
         h->P.slow_k = k ? atoi(k) : 4;  // TOI events of an env's step that make it slow (the cap always does)
     }
-    h->P.list_overflow = h->phys ? h->phys + n_envs + 3 : nullptr;
+    h->P.list_overflow = h->phys ? h->phys + list_ints + 3 : nullptr;
     h->slow = nullptr;
     h->slow_flag = nullptr;
     if (e == hipSuccess) e = hipMalloc(&h->slow, ((size_t)n_envs + 4) * sizeof(int));
@@ -611,8 +619,8 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
     h->P.solve_one_lane = 0;
     h->P.toi_diag = nullptr;
 #ifdef MAS_PROFILE
-    if (e == hipSuccess) e = hipMalloc(&h->P.prof, 64 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(h->P.prof, 0, 64 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&h->P.prof, kProfWords * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(h->P.prof, 0, kProfWords * sizeof(unsigned long long));
 #endif
     if (e != hipSuccess) {
         std::string msg = std::string("mas_create: ") + hipGetErrorString(e);
@@ -646,14 +654,15 @@ int mas_destroy(mas_handle* h)
 }
 
 #ifdef MAS_PROFILE
-// profiling build only (not part of the ABI): copy out and clear the per-phase
-// wave-time accumulators (units: 10 ns ticks of the 100 MHz constant clock).
+// profiling build only (not part of the ABI): copy out and clear the per-wave
+// phase records, kProfWords 8-B words (mas_env.h; units: 10 ns ticks of the
+// 100 MHz constant clock).
 int mas_prof_read(mas_handle* h, unsigned long long* host64)
 {
     if (!h || !host64 || !h->P.prof) return fail(MAS_ERR_INVALID_ARG, "mas_prof_read: not a profiling build");
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(host64, h->P.prof, 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemset(h->P.prof, 0, 64 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemcpy(host64, h->P.prof, kProfWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(h->P.prof, 0, kProfWords * sizeof(unsigned long long)));
     return MAS_OK;
 }
 #endif

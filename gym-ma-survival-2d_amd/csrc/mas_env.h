@@ -91,6 +91,13 @@ struct Params {
     int* phys_list;   // envs that left the contact-free fast path this step (k_pre -> general path)
     int* phys_count;  // number of them: appended by k_pre, zeroed by the first post kernel on the caller's
                       // stream once the general path (its only reader) is done (graph-replay safe)
+    // The general-path list in list_shards shards (kListShards, or 1): k_pre
+    // block b appends to shard b % list_shards -- its entries at
+    // phys_list[shard * list_cap ..], its count at phys_count[shard *
+    // kShardStride] -- so that no single counter takes every wave's atomic
+    // (memory-side atomics on one address serialise: round 4's one counter
+    // cost k_pre ~17 us per wave in the PPO regime, profiles/r05e_prof_env_ppo.txt)
+    int list_shards, list_cap;
     int* phys_last;   // the last step's count, copied there before the zeroing (mas_debug_counters)
     int* list_overflow;  // appends to phys_list / slow_list / reset_list refused by their bounds (mas_debug_guards)
     int* reset_list;     // [N] the done envs of this step's post kernel (auto-reset; the side stream: its own list)
@@ -119,6 +126,10 @@ struct Params {
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
 };
 
+constexpr int kListShards = 64;   // shards of the general-path list (Params::list_shards)
+constexpr int kShardStride = 64;  // ints between two shard counters (256 B: their own lines)
+constexpr int kListSlack = kListShards * 64;  // list entries allocated past N (the shards' rounding)
+
 // The slow split (launch_step): a second stream of the handle for the slow
 // list's general path and post phases, forked from and joined back into the
 // caller's stream by two events.  Null: the one-stream order.
@@ -127,37 +138,65 @@ struct StepSplit {
     hipEvent_t fork, join;
 };
 
-// Phase timing for the profiling build (make prof -> libmas_prof.so): lane 0
-// of each wave adds the constant-clock (100 MHz) time since the previous mark
-// to P.prof[k].  Marks sit only at wave-convergent points of k_step.
+// Phase timing for the profiling build (make prof -> libmas_prof.so): the
+// first active lane of each wave adds the constant-clock (100 MHz) time since
+// the previous mark to its workgroup's LDS accumulator of phase k (every env
+// kernel's workgroup is one wave); MAS_PROF_FLUSH(P, kid, base) at the
+// kernel's end adds the wave's phases base .. base + 13 to its own record,
+// P.prof[kProfHead + (kid * kProfBlocks + block) * 16 + q], with plain loads
+// and stores (slot 14: the wave's span since MAS_PROF(P, -1), slot 15: the
+// wave count); the host sums the records (profiles/prof_env.py).  Launches
+// that can run at the same time (the two streams of the slow split) use
+// different kids.  No atomics: round 4's marks added to one
+// global counter per phase at every mark, and those contended memory-side
+// atomics sat inside the timed phases.  Marks sit only at wave-convergent
+// points.  Phase slots: 0-5, 7 / 8-13 the general path's world steps 1 / 2
+// (kid 0; the slow list's, gen_sparse, kid 4); 20-25 k_pre_lanes (kid 1);
+// 41-45 k_post_lanes (kid 2; over a list, kid 5); 37-40 k_obs (kid 3).
+constexpr int kProfHead = 64, kProfKernels = 6, kProfBlocks = 16384;
+constexpr int kProfWords = kProfHead + kProfKernels * kProfBlocks * 16;  // 8-B words of P.prof
 #ifdef MAS_PROFILE
+constexpr int kProfSlots = 48;
+struct ProfLds {
+    unsigned long long t_last, t0;
+    unsigned long long acc[kProfSlots];
+};
+__device__ __forceinline__ ProfLds& prof_lds()
+{
+    __shared__ ProfLds s;
+    return s;
+}
+__device__ __forceinline__ bool prof_lead() { return (int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1; }
 __device__ __forceinline__ void prof_mark(const Params& P, int k)
 {
-    __shared__ unsigned long long t_last;
-    unsigned long long t = wall_clock64();
-    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) {  // first active lane
-        if (k >= 0) atomicAdd(&P.prof[k], t - t_last);
-        t_last = t;
+    const unsigned long long t = wall_clock64();
+    ProfLds& s = prof_lds();
+    if (prof_lead()) {
+        if (k < 0) {
+            for (int q = 0; q < kProfSlots; ++q) s.acc[q] = 0ull;
+            s.t0 = t;
+        } else {
+            s.acc[k] += t - s.t_last;
+        }
+        s.t_last = t;
+    }
+}
+__device__ __forceinline__ void prof_flush(const Params& P, int kid, int base)
+{
+    const unsigned long long t = wall_clock64();
+    ProfLds& s = prof_lds();
+    if (prof_lead() && blockIdx.x < (unsigned)kProfBlocks) {
+        unsigned long long* rec = P.prof + kProfHead + ((int64_t)kid * kProfBlocks + blockIdx.x) * 16;
+        for (int q = 0; q < 14; ++q) rec[q] += base + q < kProfSlots ? s.acc[base + q] : 0ull;
+        rec[14] += t - s.t0;
+        rec[15] += 1ull;
     }
 }
 #define MAS_PROF(P, k) ::mas::prof_mark(P, k)
-// a wave's whole span from t0: its max (P.prof[62]) and a histogram in 10-us
-// buckets (P.prof[48 + min(span / 10 us, 13)])
-__device__ __forceinline__ void prof_span(const Params& P, unsigned long long t0)
-{
-    const unsigned long long d = wall_clock64() - t0;
-    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) {
-        atomicMax(&P.prof[62], d);
-        const unsigned long long b = d / 1000ull;
-        atomicAdd(&P.prof[48 + (b < 13ull ? b : 13ull)], 1ull);
-    }
-}
-#define MAS_PROF_T0(v) const unsigned long long v = wall_clock64()
-#define MAS_PROF_SPAN(P, v) ::mas::prof_span(P, v)
+#define MAS_PROF_FLUSH(P, kid, base) ::mas::prof_flush(P, kid, base)
 #else
-#define MAS_PROF_T0(v) ((void)0)
-#define MAS_PROF_SPAN(P, v) ((void)0)
 #define MAS_PROF(P, k) ((void)0)
+#define MAS_PROF_FLUSH(P, kid, base) ((void)0)
 #endif
 enum ProfPhase { kPfLoad, kPfCollide, kPfSolve, kPfToi, kPfStore, kPfCount };
 

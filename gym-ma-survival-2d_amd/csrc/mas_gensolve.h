@@ -303,7 +303,7 @@ __device__ __forceinline__ void island_solve_regs(const Params& P, const SolveRe
 #endif
 template <class C, bool TOI>
 __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __restrict__ state, int64_t N, int64_t e,
-                                                bool valid, int s, float* rec_lds, int slot)
+                                                bool valid, int s, float* rec_lds, int slot, int pf = 0)
 {
     using SS = SolveShape<C>;
     using TW = StateWords<C>;
@@ -374,7 +374,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
     }
     const float inv_dt = 1.0f / dt;
     const float dtRatio = inv_dt0 * dt;
-    MAS_PROF(P, kPfLoad);
+    MAS_PROF(P, pf + kPfLoad);
 
     // ---------------- Collide: agent-agent pairs (serial on every lane) ----------------
     uint32_t aat = aat0, aa_eval = 0;
@@ -438,7 +438,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
         const bool ev = bit(alive, i) && bit(awake, i);
         ast[i] = ev ? ((lost ? 0u : (ast0[i] & ~low)) | tb) : ast0[i];
     }
-    MAS_PROF(P, kPfCollide);
+    MAS_PROF(P, pf + kPfCollide);
 
     // ---------------- Solve: islands (uniform), wake, damping ----------------
     int label[AM];
@@ -739,7 +739,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             }
         }
     }
-    MAS_PROF(P, kPfSolve);
+    MAS_PROF(P, pf + kPfSolve);
     const uint32_t awake_fin = (awake_pre & ~solved) | group_or<G>(new_awake);
     uint32_t toi_ran = 0;
     int toi_events = 0;  // TOI events of the env's agents, + 65536 per capped agent
@@ -759,7 +759,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
         // the island solve's impulse stores are ordered before SolveTOI's
         // impulse resets (the same words, other lanes of this wave)
         __threadfence_block();
-        MAS_PROF(P, kPfSolve);
+        MAS_PROF(P, pf + 5);  // the bodies' shuffles + the fence's wait for the impulse stores
         // ---------------- b2World::SolveTOI, agent by agent on the group ----------------
         // (TOI events of different agents are independent: statics never
         // move, agent-agent pairs are not TOI pairs.)  An agent whose sweep
@@ -825,7 +825,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             toi_ran |= 1u << i;
             if (P.toi_diag && o.events && s == 0 && valid) atomicAdd(P.toi_diag + e, o.events);
         }
-        MAS_PROF(P, kPfToi);
+        MAS_PROF(P, pf + kPfToi);
         // a slow env (sub-step cap, or many events) takes the slow list next
         // step (k_pre); the flag was cleared by this step's k_pre
         if (valid && s == 0 && P.slow_k > 0 && ((toi_events >> 16) != 0 || (toi_events & 0xffff) >= P.slow_k)) {
@@ -860,7 +860,7 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
         sw[1] = c0s.y;
         sw[2] = sel(as_, s);
     }
-    MAS_PROF(P, kPfStore);
+    MAS_PROF(P, pf + kPfStore);
 }
 
 }  // namespace mas

@@ -339,11 +339,17 @@ __device__ __forceinline__ bool world_step_fast_lane(AgentL<C>& g, bool alive, b
         const float rad = P.agent_r + P.agent_r;
         if (!(dot(d, d) > rad * rad)) bail = true;
     }
-    // agent-static pairs: any narrowphase candidate -> general path
+    // agent-static pairs: any narrowphase candidate -> general path.  (Over
+    // the class maxima with the count as the guard: every static's index is
+    // a constant -- a wall's bounds come straight from P, a box's LDS reads
+    // issue up front -- instead of a runtime loop selecting among the walls;
+    // the same tests, so the same decision.)
     const int ns = kNumWalls + V.nbox();
     const float reach = P.agent_r + kPolyRadius + 1e-3f;
     if (alive && awake) {
-        for (int s = 0; s < ns; ++s) {
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (s >= ns) continue;
             V2 lo, hi;
             static_v(V, P, s, lo, hi);
             const float dx = fmaxf(fmaxf(lo.x - g.c.x, g.c.x - hi.x), 0.0f);
@@ -382,10 +388,19 @@ __device__ __forceinline__ bool world_step_fast_lane(AgentL<C>& g, bool alive, b
             1.4143f * ((kPolyRadius + P.agent_r - 3.0f * kLinearSlop) + 0.25f * kLinearSlop + 0.02f) + 0.05f;
         const V2 slo = mk(fminf(c0.x, g.c.x) - Rp, fminf(c0.y, g.c.y) - Rp);
         const V2 shi = mk(fmaxf(c0.x, g.c.x) + Rp, fmaxf(c0.y, g.c.y) + Rp);
-        for (int s = 0; s < ns; ++s) {
+        // (the cull over the class maxima, constant indices; the exact
+        // reject for the surviving statics, by runtime index)
+        uint32_t near = 0;
+#pragma unroll
+        for (int s = 0; s < C::NS; ++s) {
+            if (s >= ns) continue;
             V2 lo, hi;
             static_v(V, P, s, lo, hi);
-            if (slo.x > hi.x || shi.x < lo.x || slo.y > hi.y || shi.y < lo.y) continue;
+            if (!(slo.x > hi.x || shi.x < lo.x || slo.y > hi.y || shi.y < lo.y)) near |= 1u << s;
+        }
+        while (near) {
+            const int s = __builtin_ctz(near);
+            near &= near - 1u;
             const StaticG sg = static_geom_v(V, P, s);
             if (!toi_reject(sg, c0, g.c, P.agent_r)) bail = true;
         }
@@ -770,19 +785,23 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
         const bool mine = lead && !ok && slow == (q == 1);
         const uint64_t m = __ballot(mine);
         if (m == 0ull) continue;
-        int* list = q ? P.slow_list : P.phys_list;
-        int* count = q ? P.slow_count : P.phys_count;
+        // the general-path list: this block's shard (Params::list_shards)
+        const int sh = q ? 0 : (int)(blockIdx.x % (unsigned)P.list_shards);
+        int* list = q ? P.slow_list : P.phys_list + (int64_t)sh * P.list_cap;
+        int* count = q ? P.slow_count : P.phys_count + sh * kShardStride;
+        const int64_t cap = q ? N : (int64_t)P.list_cap;
         const int leader = __ffsll((unsigned long long)m) - 1;
         int base = 0;
         if (lane == leader) base = atomicAdd(count, __popcll(m));
         base = __shfl(base, leader, 64);
         if (mine) {
             const int64_t at = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
-            if (at < N) list[at] = (int)e;
+            if (at < cap) list[at] = (int)e;
             else atomicAdd(P.list_overflow, 1);
         }
     }
     MAS_PROF(P, 25);
+    MAS_PROF_FLUSH(P, 1, 20);
 }
 
 }  // namespace mas

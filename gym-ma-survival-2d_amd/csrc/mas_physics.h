@@ -760,34 +760,18 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
     const int lane = (int)(threadIdx.x & 63);
     const int base = lane & ~(G - 1);
     const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << base;
-#ifdef MAS_PROFILE
-    // per group: TOI calls, position iterations, phase times (constant clock)
-    unsigned long long ntoi = 0, npos = 0, lt = wall_clock64(), tp[5] = {0, 0, 0, 0, 0};
-#define MAS_GT(k)                                     \
-    do {                                              \
-        const unsigned long long n_ = wall_clock64(); \
-        tp[k] += n_ - lt;                             \
-        lt = n_;                                      \
-    } while (0)
-#else
-#define MAS_GT(k) ((void)0)
-#endif
     for (int guard = 0; guard < 9 * C::NS + 1; ++guard) {
         // (1) this lane's stale TOI: conservative pre-test, else b2TimeOfImpact
         if (mine && en && cnt <= 8 && !val) {
             float alpha = 1.0f;
             if (!toi_reject(g, sw.c0, sw.c, r)) {
                 float beta;
-#ifdef MAS_PROFILE
-                ++ntoi;
-#endif
                 const int st = time_of_impact(T, sw, r, beta);
                 if (st == kToiTouching) alpha = fmin_b2(sw.alpha0 + (1.0f - sw.alpha0) * beta, 1.0f);
             }
             toi = alpha;
             val = true;
         }
-        MAS_GT(0);
         // (2) group minimum over the candidates with alpha < 1
         float ma = (mine && en && cnt <= 8 && toi < 1.0f) ? toi : 2.0f;
         int ms = s;
@@ -863,15 +847,11 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
             spp[j] = mk(gshfl<G>(ppt.x, q), gshfl<G>(ppt.y, q));
             ssp[j] = mk(gshfl<G>(g.p.x, q), gshfl<G>(g.p.y, q));
         }
-        MAS_GT(1);
         V2 cB = sw.c;
         float aB = sw.a;
         if (nsl <= NSLOT && !MAS_TOI_FORCE_FALLBACK) {
             // b2Island::SolveTOI: position iterations (TOI Baumgarte) ...
             for (int it = 0; it < 20; ++it) {
-#ifdef MAS_PROFILE
-                ++npos;
-#endif
                 const V2 cp = cB;
                 const float ap = aB;
                 float minsep = 0.0f;
@@ -884,7 +864,6 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                 if (minsep >= -1.5f * kLinearSlop) break;
                 if (same_bits(cB, cp) && same_bits(aB, ap)) break;  // fixed point (see same_bits)
             }
-            MAS_GT(2);
             sw.c0 = cB;
             sw.a0 = aB;
             // ... then 10 velocity iterations without warm starting
@@ -928,9 +907,6 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
             // registers for the whole kernel
 #pragma unroll 1
             for (int it = 0; it < 20; ++it) {
-#ifdef MAS_PROFILE
-                ++npos;
-#endif
                 const V2 cp = cB;
                 const float ap = aB;
                 float minsep = 0.0f;
@@ -945,7 +921,6 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                 if (minsep >= -1.5f * kLinearSlop) break;
                 if (same_bits(cB, cp) && same_bits(aB, ap)) break;  // fixed point (see same_bits)
             }
-            MAS_GT(2);
             sw.c0 = cB;
             sw.a0 = aB;
             VC km = vc_init_as_h(nm, pm, sm, cB, r, m, Ii);
@@ -976,13 +951,11 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
                 }
             }
         }
-        MAS_GT(3);
         const float h = (1.0f - minAlpha) * dt;
         integrate(cB, aB, vB, wB, h);
         sw.c = cB;
         sw.a = aB;
         val = false;
-        MAS_GT(4);
     }
     ToiGroupOut o;
     o.c = sw.c;
@@ -992,24 +965,6 @@ __device__ __forceinline__ ToiGroupOut toi_agent_group(const EnvL<C>& L, const P
     o.touch = (uint32_t)((__ballot(mine && touch) & gmask) >> base);
     const bool capped = (__ballot(mine && en && cnt > 8) & gmask) != 0ull;
     o.events = events + (capped ? 65536 : 0);
-#ifdef MAS_PROFILE
-    // same slots as toi_agent's profile (profiles/prof_toi.py): max per group
-    // of events / TOI calls (summed over the group's lanes) / position
-    // iterations, totals, and the longest time per phase (0 TOI, 1 min +
-    // narrowphase + island gather, 2 position, 3 velocity, 4 integrate)
-    unsigned long long gt = ntoi;
-#pragma unroll
-    for (int o2 = 1; o2 < G; o2 <<= 1) gt += __shfl_xor(gt, o2, 64);
-    if (s == 0) {
-        atomicMax(&P.prof[48], (unsigned long long)events);
-        atomicMax(&P.prof[49], gt);
-        atomicMax(&P.prof[50], npos);
-        atomicAdd(&P.prof[51], (unsigned long long)events);
-        atomicAdd(&P.prof[52], gt);
-        for (int k = 0; k < 5; ++k) atomicMax(&P.prof[53 + k], tp[k]);
-    }
-#endif
-#undef MAS_GT
     return o;
 }
 

@@ -1158,10 +1158,17 @@ __device__ __forceinline__ void copy_db(bf8* __restrict__ buf, const bf8* __rest
 }
 // the stage copied one phase ago has landed in every wave: NST = this wave's
 // vector memory operations issued after those copies (a lower bound)
+// (the s_movk_i32 of 0x7a00 + NST into a dead SGPR marks the wait in the ISA:
+// scripts/check_policy_waits.py, run by __graft_entry__.build(), checks that
+// at least min(NST, 63) vector memory instructions follow the last copy
+// before every marker -- a count above the real one would stop waiting
+// before the copies land)
 template <int NST>
 __device__ __forceinline__ void land_db()
 {
     constexpr int n = NST > 63 ? 63 : NST;
+    int mark;
+    asm volatile("s_movk_i32 %0, %1" : "=s"(mark) : "n"(0x7a00 + n));
     __builtin_amdgcn_s_waitcnt((n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8));
     lds_barrier();
 }

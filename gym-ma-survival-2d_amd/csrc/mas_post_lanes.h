@@ -1549,6 +1549,7 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
     (void)rr;
 #endif
     MAS_PROF(P, 45);
+    MAS_PROF_FLUSH(P, M == kGenEnvs ? 5 : 2, 41);
 }
 
 }  // namespace mas

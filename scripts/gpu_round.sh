@@ -1,8 +1,8 @@
 #!/bin/bash
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
-#   tests t:<files> ab smoke bench env full profd envprof pmc pmcenv profgen
-#   proflanes splitab libab:<variant>)
+#   tests t:<files> ab smoke bench env full profd envprof pmc pmcenv profenv
+#   libab:<variant>)
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
 R=$GRAFT_REPO_ROOT
@@ -68,20 +68,10 @@ for step in "$@"; do
         python3 $R/bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/prof_ffa.log 2>&1 || exit $?
       cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_1v1 -o run -- \
         python3 $R/bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline > $O/prof_1v1.log 2>&1 || exit $? ;;
-    profk)
-      cd $R && timeout -k 10 300 python -u profiles/prof_kernels.py 65536 20 > $O/prof_kernels.log 2>&1 || exit $? ;;
-    profgen)
-      cd $R && timeout -k 10 300 python -u profiles/prof_toi.py 65536 4 > $O/prof_toi.log 2>&1 || exit $?
-      cd $R && timeout -k 10 300 python -u profiles/prof_general.py 65536 20 --ppo > $O/prof_general.log 2>&1 || exit $? ;;
-    splitab)
-      # MAS_SPLIT A/B (same box, alternating processes): driver window and env-only 2v2 / FFA4
-      for sp in 2 3 2 3; do
-        cd $R && MAS_SPLIT=$sp timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/splitab_driver_sp$sp.json 2>> $O/splitab.err || exit 1
-      done
-      for sp in 2 3 2 3; do
-        cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline >> $O/splitab_env_sp$sp.json 2>> $O/splitab.err || exit 1
-        cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline >> $O/splitab_ffa_sp$sp.json 2>> $O/splitab.err || exit 1
-      done ;;
+    profenv)
+      # phase timers of the env kernels (libmas_prof.so, `make -C gym-ma-survival-2d_amd/csrc prof`)
+      cd $R && timeout -k 10 300 python -u profiles/prof_env.py 2v2 65536 20 --ppo > $O/prof_env_ppo.txt 2>&1 || exit $?
+      cd $R && timeout -k 10 200 python -u profiles/prof_env.py 2v2 65536 20 > $O/prof_env_2v2.txt 2>&1 || exit $? ;;
     libab:*)
       # libab:<variant>: driver window + env-only 2v2, default library vs masurvival/_lib/libmas_<variant>.so, alternating
       V=${step#libab:}
@@ -101,14 +91,6 @@ for step in "$@"; do
             -d $O/pmc_${c}_$1_$2 -o run -- python3 $R/bench.py --mode env --config $1 --envs $2 --steps $3 --warmup $4 --no-cpu-baseline > $O/pmc_${c}_$1_$2.log 2>&1 || exit 1
         done
       done ;;
-    profsplit)
-      # kernel traces of the driver window under MAS_SPLIT 2 and 3 (profiles/timeline.py)
-      for sp in 2 3; do
-        cd /tmp && MAS_SPLIT=$sp timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sp$sp -o run -- \
-          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_sp$sp.log 2>&1 || exit $?
-      done ;;
-    proflanes)
-      cd $R && timeout -k 10 200 python -u profiles/prof_lanes.py 2v2 65536 20 > $O/prof_lanes_2v2.txt 2>&1 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"

@@ -56,3 +56,17 @@ def test_create_rejects_unknown_split_mode_without_gpu(val, monkeypatch):
     rc = lib.mas_create(ctypes.byref(cfg), 4, 0, ctypes.byref(h))
     assert rc == -1
     assert b'MAS_SPLIT' in lib.mas_last_error()
+
+
+def test_policy_counted_waits_cover_their_copies():
+    """k_policy_train_db's land_db<NST> waits: in the built ISA at
+    least min(NST, 63) vector memory instructions follow the copies each one
+    waits for (scripts/check_policy_waits.py, also run by build())."""
+    import subprocess
+    import sys
+    if not os.path.exists(abi.LIB_PATH) or not os.path.exists('/opt/rocm/lib/llvm/bin/llvm-objdump'):
+        pytest.skip('library or llvm-objdump absent')
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'scripts', 'check_policy_waits.py')],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert 'counted waits OK' in r.stdout
