@@ -516,7 +516,7 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
         else if (!strcmp(v, "2")) split_mode = 2;
         else
             return fail(MAS_ERR_INVALID_ARG, "mas_create: MAS_SPLIT must be 0 (one stream) or 2 (the slow split); "
-                                             "modes 1 and 3 were removed");
+                                             "modes 1 and 3 were removed (DESIGN.md 4.1.1)");
     }
     mas_handle* h = new (std::nothrow) mas_handle();
     if (!h) return fail(MAS_ERR_OOM, "mas_create: out of host memory");
@@ -857,7 +857,7 @@ int mas_debug_force_general(mas_handle* h, int32_t on)
 #if !MAS_AB_KERNELS
     if (on & 2) return fail(MAS_ERR_UNSUPPORTED, "mas_debug_force_general: the one-lane kernels are in libmas_ab.so only");
 #endif
-    if (on & 4) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: bit 2 (the all-general split) was removed");
+    if (on & 4) return fail(MAS_ERR_INVALID_ARG, "mas_debug_force_general: bit 2 (the general split) was removed");
     h->P.force_general = (on & 1) ? 1 : 0;
     h->P.solve_one_lane = (on & 2) ? 1 : 0;
     h->split = (on & 8) ? 0 : h->split_default;

@@ -289,6 +289,102 @@ __device__ __forceinline__ void island_solve_regs(const Params& P, const SolveRe
     }
 }
 
+// island_solve_regs for an island of ONE body (agent r) and n <= KC contacts,
+// all agent-static: the body stays in scalars instead of being selected out
+// of and put back into the AM-wide arrays around every contact of every
+// iteration.  The same operations on the same values in the same order
+// (the other bodies never change, so the fixed-point test over all of them
+// reduces to body r and the contacts), so the same bits.
+template <class C, class KT>
+__device__ __forceinline__ void island_solve_one(const Params& P, const SolveRec<C>& R, const KT& K,
+                                                 const int (&qi)[SolveShape<C>::KR], int n, int r, V2& c, float& a,
+                                                 V2& v, float& w, float& sl, float dt, bool& asleep)
+{
+    constexpr int KC = SolveShape<C>::KR;
+    const float m = P.inv_mass, Ii = P.inv_I;
+    VC k[KC];
+    V2 pn[KC], pp[KC];
+    int js[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        const int q = j < n ? qi[j] : 0;
+        k[j].normal = mk(R.at(kRnx, q), R.at(kRny, q));
+        k[j].rA = mk(R.at(kRax, q), R.at(kRay, q));
+        k[j].rB = mk(R.at(kRbx, q), R.at(kRby, q));
+        k[j].nm = R.at(kRnm, q);
+        k[j].tm = R.at(kRtm, q);
+        k[j].ni = R.at(kRni, q);
+        k[j].ti = R.at(kRti, q);
+        js[j] = slot_js(__float_as_int(R.at(kRkey, q)));
+        pn[j] = mk(R.at(kRpnx, q), R.at(kRpny, q));
+        pp[j] = mk(R.at(kRppx, q), R.at(kRppy, q));
+    }
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        if (j >= n) continue;
+        V2 vA = mk(0.0f, 0.0f);
+        float wA = 0.0f;
+        vc_warm(k[j], vA, wA, v, w, 0.0f, 0.0f, m, Ii);
+    }
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        const V2 vp = v;
+        const float wp = w;
+        float qn[KC], qt[KC];
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            qn[j] = k[j].ni;
+            qt[j] = k[j].ti;
+        }
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            if (j >= n) continue;
+            V2 vA = mk(0.0f, 0.0f);
+            float wA = 0.0f;
+            vc_solve(k[j], vA, wA, v, w, 0.0f, 0.0f, m, Ii);
+        }
+        bool same = same_bits(v, vp) && same_bits(w, wp);
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+            if (j < n) same = same && same_bits(k[j].ni, qn[j]) && same_bits(k[j].ti, qt[j]);
+        if (same) break;
+    }
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        if (j >= n) continue;
+        K.set_asni(r, js[j], k[j].ni);
+        K.set_asti(r, js[j], k[j].ti);
+    }
+    integrate(c, a, v, w, dt);
+    bool converged = false;
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        float minsep = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            if (j >= n) continue;
+            minsep = fmin_b2(minsep, pc_solve_as_h(pn[j], pp[j], c, a, P.agent_r, m, Ii, kBaumgarte, P.inv_mass_rcp));
+        }
+        if (minsep >= -3.0f * kLinearSlop) {
+            converged = true;
+            break;
+        }
+    }
+    // sleep (island_solve_regs' loop for the one member)
+    const float linTolSqr = kLinSleepTol * kLinSleepTol;
+    const float angTolSqr = kAngSleepTol * kAngSleepTol;
+    const bool moving = (w * w > angTolSqr) | (dot(v, v) > linTolSqr);
+    const float acc = opq(sl + dt);
+    sl = moving ? 0.0f : acc;
+    const float ms = moving ? 0.0f : fmin_b2(kMaxFloat, acc);
+    asleep = ms >= kTimeToSleep && converged;
+    if (asleep) {
+        sl = 0.0f;
+        v = mk(0.0f, 0.0f);
+        w = 0.0f;
+    }
+}
+
 // One world step's Collide + Solve of env e on this lane's group (lane s of
 // the group).  valid: the group holds an env (every lane of the wave runs the
 // ballots and the barrier).  rec: this workgroup's contact records.
@@ -574,7 +670,19 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             for (int j = 0; j < KC; ++j) qi[j] = opq(j == nqi ? q : qi[j]);
             ++nqi;
         }
-        if (nqi <= KC) {
+        if (nqi <= KC && members == (1u << r)) {
+            // one body (every contact agent-static): scalars, no selects
+            V2 cr = sel(c, r), vr = sel(v, r);
+            float ar = sel(a, r), wr = sel(w, r), slr = sel(sl, r);
+            bool asleep;
+            island_solve_one<C>(P, R, K, qi, nqi, r, cr, ar, vr, wr, slr, dt, asleep);
+            put(c, r, cr);
+            put(a, r, ar);
+            put(v, r, vr);
+            put(w, r, wr);
+            put(sl, r, slr);
+            new_awake = asleep ? 0u : members;
+        } else if (nqi <= KC) {
             island_solve_regs<C>(P, R, K, qi, nqi, members, c, a, v, w, sl, dt, new_awake);
         } else {
         auto load_vc = [&](int q) {

@@ -965,11 +965,19 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
     const int A = P.A;
     // the env of slot j (lanes past the last env, or of an env the other
     // stream owns, stay for the wave's collectives and store nothing)
-    const int64_t cnt = gen_list_count<M>(P, N);
     const int64_t k0 = (int64_t)blockIdx.x * S;
-    if (M == kGenEnvs && k0 >= cnt) return;  // the whole workgroup (one wave)
-    bool valid = k0 + j < cnt;
-    const int64_t e = M == kGenEnvs ? (int64_t)P.phys_list[valid ? k0 + j : k0] : (valid ? k0 + j : N - 1);
+    bool valid;
+    int64_t e;
+    if (M == kGenEnvs) {
+        // the list's entries k0 .. k0 + S - 1 (a sharded list: list_pos)
+        const ListPos lp = list_pos(P, N, k0, k0 + j);
+        if (!lp.any) return;  // the whole workgroup (one wave)
+        valid = lp.valid;
+        e = valid ? lp.e : (int64_t)P.phys_list[0];
+    } else {
+        valid = k0 + j < N;
+        e = valid ? k0 + j : N - 1;
+    }
     if (valid && other_stream<M>(P, e)) valid = false;
     if (i == 0) lds.eidx[j] = e;
     wave_lds_sync();

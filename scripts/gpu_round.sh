@@ -2,7 +2,7 @@
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
 #   tests t:<files> ab smoke bench env full profd envprof pmc pmcenv profenv
-#   libab:<variant>)
+#   split0ab libab:<variant>)
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
 R=$GRAFT_REPO_ROOT
@@ -72,6 +72,12 @@ for step in "$@"; do
       # phase timers of the env kernels (libmas_prof.so, `make -C gym-ma-survival-2d_amd/csrc prof`)
       cd $R && timeout -k 10 300 python -u profiles/prof_env.py 2v2 65536 20 --ppo > $O/prof_env_ppo.txt 2>&1 || exit $?
       cd $R && timeout -k 10 200 python -u profiles/prof_env.py 2v2 65536 20 > $O/prof_env_2v2.txt 2>&1 || exit $? ;;
+    split0ab)
+      # the slow split (default) vs one stream (MAS_SPLIT=0), alternating processes: driver window, env-only 2v2
+      for sp in 2 0 2 0; do
+        cd $R && MAS_SPLIT=$sp timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/split0ab_driver_sp$sp.json 2>> $O/split0ab.err || exit 1
+        cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline >> $O/split0ab_env_sp$sp.json 2>> $O/split0ab.err || exit 1
+      done ;;
     libab:*)
       # libab:<variant>: driver window + env-only 2v2, default library vs masurvival/_lib/libmas_<variant>.so, alternating
       V=${step#libab:}

@@ -46,8 +46,9 @@ def test_create_rejects_bad_config_without_gpu():
 
 @pytest.mark.parametrize('val', ['1', '3', 'x'])
 def test_create_rejects_unknown_split_mode_without_gpu(val, monkeypatch):
-    """MAS_SPLIT takes 0 (one stream) or 2 (the slow split); the removed modes
-    and anything else are refused before any device allocation."""
+    """MAS_SPLIT takes 0 (one stream) or 2 (the slow split); the removed
+    modes and anything else are refused before any device allocation (ADVICE
+    r04)."""
     monkeypatch.setenv('MAS_SPLIT', val)
     lib = abi.load_library()
     from masurvival.config import ResolvedConfig
