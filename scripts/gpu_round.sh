@@ -2,7 +2,7 @@
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
 #   tests t:<files> ab smoke bench env full profd envprof pmc pmcenv profenv
-#   split0ab libab:<variant>)
+#   split0ab slowkab libab:<variant>)
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
 R=$GRAFT_REPO_ROOT
@@ -77,6 +77,11 @@ for step in "$@"; do
       for sp in 2 0 2 0; do
         cd $R && MAS_SPLIT=$sp timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/split0ab_driver_sp$sp.json 2>> $O/split0ab.err || exit 1
         cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline >> $O/split0ab_env_sp$sp.json 2>> $O/split0ab.err || exit 1
+      done ;;
+    slowkab)
+      # MAS_SLOW_K (TOI events of an env's step that send it to the slow list next step): 4 (default) vs 2 vs 1
+      for k in 4 2 1 4 2 1; do
+        cd $R && MAS_SLOW_K=$k timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/slowkab_driver_k$k.json 2>> $O/slowkab.err || exit 1
       done ;;
     libab:*)
       # libab:<variant>: driver window + env-only 2v2, default library vs masurvival/_lib/libmas_<variant>.so, alternating
