@@ -46,6 +46,9 @@ MAS_DECLARE(ffal)
 #ifdef MAS_HAVE_xl
 MAS_DECLARE(xl)
 #endif
+#ifdef MAS_HAVE_xxl
+MAS_DECLARE(xxl)
+#endif
 // fused policy MLP of the PPO consumer (mas_policy.hip)
 int64_t policy_packed_bytes(int D);
 int64_t policy_blocks(int64_t M);
@@ -542,6 +545,9 @@ int mas_create(const mas_config* cfg, int64_t n_envs, int32_t device, mas_handle
 #endif
 #ifdef MAS_HAVE_xl
     if (!ok && fits(8, 8, 8, 4)) { h->ops = Ops{class_info_xl(), launch_step_xl, launch_reset_xl, launch_view_xl}; ok = true; }
+#endif
+#ifdef MAS_HAVE_xxl
+    if (!ok && fits(8, 20, 16, 8)) { h->ops = Ops{class_info_xxl(), launch_step_xxl, launch_reset_xxl, launch_view_xxl}; ok = true; }
 #endif
     if (!ok) {
         delete h;

@@ -6,7 +6,10 @@ The `ffal` class (4 agents, 24 heals, 16 boxes, 8 inventory slots; 64 bodies,
 the limit of the 64-bit body masks) takes the 4-agent configs of the paper's
 media (8x8 grid, ~16-20 heals, ~8-12 randomized boxes, SURVEY.md section 2
 row 8) and inventories larger than 4.  Parity: every env replayed by the
-oracle with the same seeds and actions, bit-exact, with auto-reset."""
+oracle with the same seeds and actions, bit-exact, with auto-reset.
+
+The `xxl` class (8 agents, 20 heals, 16 boxes, 8 slots) takes the 5-8 agent
+configs with the larger worlds (FFA8 and 4v4 below)."""
 import numpy as np
 import pytest
 
@@ -42,10 +45,32 @@ TEAMS_BIG = {
     'inventory': {'slots': 8},
     'safe_zone': {'phases': 5, 'cooldown': 25, 'damage': 4, 'radiuses': [10, 5, 2.5, 1], 'centers': 'random'},
     'melee': MELEE}
+# the `xxl` class (8 agents, 20 heals, 16 boxes, 8 slots; 64 bodies)
+FFA8_BIG = {
+    'agents': {'n_agents': 8, 'agent_size': 1},
+    'spawn_grid': {'grid_size': 8, 'floor_size': 24},
+    'heals': {'reset_spawns': {'n_items': 20, 'item_size': 0.5}, 'heal': {'healing': 50}},
+    'boxes': {'reset_spawns': {'n_boxes': 16, 'box_size': 1}, 'ownership': False,
+              'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20,
+              'randomized_shape': {'avg_w': 1.0, 'std_w': 0.5, 'avg_h': 1.0, 'std_h': 0.5}},
+    'inventory': {'slots': 8},
+    'safe_zone': {'phases': 5, 'cooldown': 25, 'damage': 4, 'radiuses': [12, 6, 3, 1], 'centers': 'random'},
+    'melee': MELEE}
+TEAMS8_BIG = {
+    'agents': {'n_agents': 8, 'agent_size': 1}, 'teams': {'twoteams': True},
+    'spawn_grid': {'grid_size': 7, 'floor_size': 20},
+    'heals': {'reset_spawns': {'n_items': 16, 'item_size': 0.5}, 'heal': {'healing': 50}},
+    'boxes': {'reset_spawns': {'n_boxes': 12, 'box_size': 1}, 'ownership': True,
+              'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20},
+    'inventory': {'slots': 6},
+    'safe_zone': {'phases': 5, 'cooldown': 25, 'damage': 4, 'radiuses': [10, 5, 2.5, 1], 'centers': 'random'},
+    'melee': MELEE}
 
 
 @pytest.mark.parametrize('name,cfg,n,T', [('ffa4 20 heals 12 boxes 6 slots', FFA4_BIG, 256, 200),
-                                          ('2v2 24 heals 16 owned boxes 8 slots', TEAMS_BIG, 128, 200)])
+                                          ('2v2 24 heals 16 owned boxes 8 slots', TEAMS_BIG, 128, 200),
+                                          ('ffa8 20 heals 16 boxes 8 slots', FFA8_BIG, 128, 200),
+                                          ('4v4 16 heals 12 owned boxes 6 slots', TEAMS8_BIG, 128, 200)])
 def test_large_capacity_configs_match_oracle(name, cfg, n, T):
     rc = ResolvedConfig(cfg)
     try:
@@ -73,3 +98,11 @@ def test_large_capacity_configs_match_oracle(name, cfg, n, T):
             assert np.array_equal(o[e], oo), (name, t, e, gr.diff(o[e], oo))
     assert resets > 0
     env.close()
+
+
+def test_config_beyond_every_class_is_refused():
+    """More than 8 agents (the widest class) is refused by mas_create with
+    MAS_ERR_UNSUPPORTED and a message naming the compiled classes."""
+    cfg = dict(FFA8_BIG, agents={'n_agents': 9, 'agent_size': 1})
+    with pytest.raises(abi.MasError, match='no compiled capacity class'):
+        VecMaSurvival(cfg, n_envs=8, seeds=range(8), auto_reset=True)
