@@ -332,6 +332,27 @@ EPISODES = [
         'inventory': {'slots': 8},
         'safe_zone': {'phases': 5, 'cooldown': 200, 'damage': 1, 'radiuses': [16, 8, 4, 2], 'centers': 'random'},
         'melee': MELEE}, 16, 116, 1200, -3),
+    # the xxl capacity class (5-8 agents with up to 20 heals, 16 boxes, 8
+    # slots): eight hoarders in a free-for-all; a 4v4 fight with owned boxes
+    ('xxl_ffa8_s17', {
+        'agents': {'n_agents': 8, 'agent_size': 1},
+        'spawn_grid': {'grid_size': 8, 'floor_size': 22},
+        'heals': {'reset_spawns': {'n_items': 20, 'item_size': 0.5}, 'heal': {'healing': 50}},
+        'boxes': {'reset_spawns': {'n_boxes': 16, 'box_size': 1}, 'ownership': False,
+                  'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20,
+                  'randomized_shape': {'avg_w': 1.0, 'std_w': 0.5, 'avg_h': 1.0, 'std_h': 0.5}},
+        'inventory': {'slots': 8},
+        'safe_zone': {'phases': 5, 'cooldown': 200, 'damage': 1, 'radiuses': [22, 11, 5, 2], 'centers': 'random'},
+        'melee': MELEE}, 17, 117, 1200, -3),
+    ('xxl_4v4_owned_s18', {
+        'agents': {'n_agents': 8, 'agent_size': 1}, 'teams': {'twoteams': True},
+        'spawn_grid': {'grid_size': 7, 'floor_size': 20},
+        'heals': {'reset_spawns': {'n_items': 16, 'item_size': 0.5}, 'heal': {'healing': 50}},
+        'boxes': {'reset_spawns': {'n_boxes': 12, 'box_size': 1}, 'ownership': True,
+                  'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20},
+        'inventory': {'slots': 6},
+        'melee': MELEE,
+        'reward_scheme': {'r_alive': 1, 'r_dead': -1, 'r_kill': 3, 'r_death': -2}}, 18, 118, 1000, 0.8),
 ]
 
 

@@ -57,3 +57,17 @@ def test_ffal_fixtures_fill_past_four_slots():
         d, cfg = gr.load(name)
         assert int(d['max_inventory']) > 4, name
         assert int(d['max_inventory']) <= cfg['inventory']['slots'], name
+
+
+def test_xxl_fixtures_exceed_the_xl_class():
+    """The xxl-class fixtures (8 agents with more heals / boxes than the xl
+    class's 8, up to 64 bodies) are configs no smaller class takes; the FFA8
+    hoarders fill the eight inventory slots."""
+    names = [f for f in FIXTURES if f.startswith('xxl_')]
+    assert len(names) >= 2
+    for name in names:
+        d, cfg = gr.load(name)
+        assert cfg['agents']['n_agents'] == 8, name
+        assert cfg['heals']['reset_spawns']['n_items'] > 8 or cfg['boxes']['reset_spawns']['n_boxes'] > 8, name
+    d, _ = gr.load('xxl_ffa8_s17.npz')
+    assert int(d['max_inventory']) == 8
