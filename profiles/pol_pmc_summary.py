@@ -1,5 +1,5 @@
 """Per-kernel averages (per dispatch) of the rocprofv3 PMC passes that
-scripts/gpu_polpmc.sh collects over scripts/policy_bench.py.
+`scripts/gpu_round.sh <tag> polpmc` collects over scripts/policy_bench.py.
 usage: python profiles/pol_pmc_summary.py <gpurun_out/polpmc> <out.json>
 FETCH_SIZE / WRITE_SIZE are KB (reported here in bytes)."""
 import collections

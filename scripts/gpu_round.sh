@@ -1,8 +1,10 @@
 #!/bin/bash
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
-#   tests t:<files> ab smoke bench env full profd envprof pmc pmcenv profenv
-#   split0ab slowkab libab:<variant>)
+#   tests t:<files> ab regimes smoke bench benchq benchcw0 shards env full
+#   envprof2 prof profd envprof pmc pmcenv sqmix profenv split0ab slowkab
+#   libab:<variant> ktrace:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
+#   polab[:<libs>] polpmc trend[:<iterations>])
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
 R=$GRAFT_REPO_ROOT
@@ -102,6 +104,57 @@ for step in "$@"; do
             -d $O/pmc_${c}_$1_$2 -o run -- python3 $R/bench.py --mode env --config $1 --envs $2 --steps $3 --warmup $4 --no-cpu-baseline > $O/pmc_${c}_$1_$2.log 2>&1 || exit 1
         done
       done ;;
+    sqmix)
+      # SQ instruction mix of the env kernels in the driver-shaped bench (one counter set, its own run)
+      cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        --kernel-include-regex "mas::k_" --output-format csv -d $O/pmc_sq -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_sq.log 2>&1 || exit 1 ;;
+    ktrace:*)
+      # ktrace:<lib>[,<lib>...]: kernel traces of the PPO bench per library (main = libmas.so)
+      for v in $(echo ${step#ktrace:} | tr ',' ' '); do
+        LIB=""; [ "$v" != main ] && LIB="--lib $R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
+        cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$v -o run -- \
+          python3 $R/bench.py --no-cpu-baseline $LIB > $O/kt_$v.log 2>&1 || exit 1
+      done ;;
+    ktraceenv:*)
+      # ktraceenv:<config>:<steps>:<lib>[,<lib>...]: kernel traces of the env-only bench per library
+      IFS=: read -r _ CFG ST LIBS <<< "$step"
+      for v in $(echo $LIBS | tr ',' ' '); do
+        LIB=""; [ "$v" != main ] && LIB="--lib $R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
+        cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_${CFG}_$v -o run -- \
+          python3 $R/bench.py --mode env --config $CFG --steps $ST --warmup 10 --no-cpu-baseline $LIB > $O/kt_${CFG}_$v.log 2>&1 || exit 1
+      done ;;
+    dist)
+      # multi-rank rehearsal on one GPU: 2 ranks over gloo (test + bench launch path)
+      cd $R && timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 240 --timeout-method thread \
+        -p no:cacheprovider > $O/dist_test.log 2>&1 || exit 1
+      cd $R && MAS_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 16 --warmup 16 --horizon 16 --envs 4096 \
+        > $O/dist_bench2.log 2>&1 || exit 1 ;;
+    polab*)
+      # polab[:<lib>,...]: GPU policy tests, then scripts/policy_bench.py over the default library and
+      # the variant libraries (scripts/build_policy_variants.sh)
+      L=gym-ma-survival-2d_amd/masurvival/_lib
+      LIBS=""; [ "$step" != polab ] && LIBS=$(echo ${step#polab:} | tr ',' '\n' | sed "s#^#$L/libmas_#; s#\$#.so#" | tr '\n' ' ')
+      cd $R && timeout -k 10 300 python -u -m pytest tests/test_gpu_policy.py -x -q --timeout 120 --timeout-method thread \
+        -p no:cacheprovider > $O/polab_tests.log 2>&1 || exit 1
+      cd $R && timeout -k 10 300 python -u scripts/policy_bench.py $L/libmas.so $LIBS > $O/polbench.log 2>&1 || exit 1 ;;
+    polpmc)
+      # PMC passes over the policy micro-bench (default library): HBM bytes, then two SQ sets
+      L=$R/gym-ma-survival-2d_amd/masurvival/_lib
+      cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "pol::k_" --output-format csv -d $O/pol_fetch -o run -- \
+        python3 $R/scripts/policy_bench.py $L/libmas.so > $O/pol_fetch.log 2>&1 || exit 1
+      cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "pol::k_" --output-format csv -d $O/pol_write -o run -- \
+        python3 $R/scripts/policy_bench.py $L/libmas.so > $O/pol_write.log 2>&1 || exit 1
+      cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU \
+        --kernel-include-regex "k_policy" --output-format csv -d $O/pol_p1 -o run -- python3 $R/scripts/policy_bench.py $L/libmas.so > $O/pol_p1.log 2>&1 || exit 1
+      cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_INSTS_VMEM \
+        --kernel-include-regex "k_policy" --output-format csv -d $O/pol_p2 -o run -- python3 $R/scripts/policy_bench.py $L/libmas.so > $O/pol_p2.log 2>&1 || exit 1 ;;
+    trend*)
+      # trend[:<iterations>]: PPO regime over many iterations, per-iteration env step cost + kernel trace
+      IT=12; [ "$step" != trend ] && IT=${step#trend:}
+      cd $R && timeout -k 10 200 python -u scripts/ppo_breakdown.py 65536 $IT > $O/trend_breakdown.log 2>&1 || exit 1
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trend_prof -o run -- \
+        python3 $R/scripts/ppo_breakdown.py 65536 $IT > $O/trend_prof.log 2>&1 || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"
