@@ -2,8 +2,8 @@
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
 #   tests t:<files> ab regimes smoke bench benchq benchcw0 shards env full
-#   envprof2 prof profd envprof pmc pmcenv sqmix profenv split0ab slowkab
-#   libab:<variant> ktrace:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
+#   envprof2 prof profd envprof pmc pmcenv sqmix profenv profwaves split0ab slowkab
+#   libab:<variant> ktrace:<libs> ktraced:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
 #   polab[:<libs>] polpmc trend[:<iterations>])
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
@@ -74,6 +74,10 @@ for step in "$@"; do
       # phase timers of the env kernels (libmas_prof.so, `make -C gym-ma-survival-2d_amd/csrc prof`)
       cd $R && timeout -k 10 300 python -u profiles/prof_env.py 2v2 65536 20 --ppo > $O/prof_env_ppo.txt 2>&1 || exit $?
       cd $R && timeout -k 10 200 python -u profiles/prof_env.py 2v2 65536 20 > $O/prof_env_2v2.txt 2>&1 || exit $? ;;
+    profwaves)
+      # per-wave span distribution of the env kernels (profiling build), PPO and random regimes
+      cd $R && timeout -k 10 300 python -u profiles/prof_env.py 2v2 65536 20 --ppo --waves > $O/prof_waves_ppo.txt 2>&1 || exit $?
+      cd $R && timeout -k 10 200 python -u profiles/prof_env.py 2v2 65536 20 --waves > $O/prof_waves_2v2.txt 2>&1 || exit $? ;;
     split0ab)
       # the slow split (default) vs one stream (MAS_SPLIT=0), alternating processes: driver window, env-only 2v2
       for sp in 2 0 2 0; do
@@ -114,6 +118,13 @@ for step in "$@"; do
         LIB=""; [ "$v" != main ] && LIB="--lib $R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
         cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$v -o run -- \
           python3 $R/bench.py --no-cpu-baseline $LIB > $O/kt_$v.log 2>&1 || exit 1
+      done ;;
+    ktraced:*)
+      # ktraced:<lib>[,<lib>...]: kernel traces of the driver-window bench (20 steps, 1 update) per library
+      for v in $(echo ${step#ktraced:} | tr ',' ' '); do
+        LIB=""; [ "$v" != main ] && LIB="--lib $R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
+        cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktd_$v -o run -- \
+          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline $LIB > $O/ktd_$v.log 2>&1 || exit 1
       done ;;
     ktraceenv:*)
       # ktraceenv:<config>:<steps>:<lib>[,<lib>...]: kernel traces of the env-only bench per library
