@@ -7,7 +7,11 @@ and the mean wave span, per kernel, over `steps` steps.
 Regimes: --ppo (2 PPO iterations of pre-roll, then rollout steps of the
 trained policy: the headline bench's regime) or random actions after 150
 steps (default).
-usage: python profiles/prof_env.py [config] [n_envs] [steps] [--ppo]"""
+With --waves: the records are read (and zeroed) after every step, so
+each active wave's own span is known; printed per kernel: the span
+percentiles per step (the launch lasts as long as its slowest wave) and the
+phases of the slowest 1 % of waves beside the mean.
+usage: python profiles/prof_env.py [config] [n_envs] [steps] [--ppo] [--waves]"""
 import ctypes
 import os
 import sys
@@ -53,15 +57,32 @@ def main():
     env = VecMaSurvival(NAMED_CONFIGS[cfg_name], n_envs=n, auto_reset=True)
     buf = (ctypes.c_ulonglong * PROF_WORDS)()
     gen_envs = 0
+    per_step = []  # --waves: each step's records (differenced)
+    prev = [None]
+    total = [None]
+
+    def snap():
+        if '--waves' not in sys.argv:
+            return
+        torch.cuda.synchronize()
+        abi.check(lib.mas_prof_read(env._h, buf))
+        # (mas_prof_read returns the records since the last read and zeroes them)
+        cur = np.frombuffer(buf, dtype=np.uint64).copy()
+        if prev[0] is not None:
+            per_step.append(cur[PROF_HEAD:].astype(np.float64).reshape(PROF_KERNELS, PROF_BLOCKS, 16))
+            total[0] = cur if total[0] is None else total[0] + cur
+        prev[0] = cur
     if '--ppo' in sys.argv:
         from masurvival.ppo import PPOConfig, PPOTrainer
         tr = PPOTrainer(env, PPOConfig(), seed=0)
         for _ in range(2):
             tr.iteration()
+        snap()
         abi.check(lib.mas_prof_read(env._h, buf))
         for t in range(steps):
             tr.rollout_step(t)
             gen_envs += env.debug_counters()['phys_general_envs']
+            snap()
         regime = 'PPO regime (after 2 iterations)'
     else:
         env.reset()
@@ -71,14 +92,16 @@ def main():
         acts = lambda: (torch.rand((n, env.n_agents, 6), generator=gen, device=env.device) * hi).to(torch.int8)  # noqa
         for _ in range(150):
             env.step(acts())
+        snap()
         abi.check(lib.mas_prof_read(env._h, buf))
         for _ in range(steps):
             env.step(acts())
             gen_envs += env.debug_counters()['phys_general_envs']
+            snap()
         regime = 'random actions (after 150 steps)'
     torch.cuda.synchronize()
     abi.check(lib.mas_prof_read(env._h, buf))
-    raw = np.frombuffer(buf, dtype=np.uint64)
+    raw = np.frombuffer(buf, dtype=np.uint64) if total[0] is None else total[0]
     print(f'# {int(np.count_nonzero(raw))} nonzero words of {raw.size}')
     rec = raw[PROF_HEAD:].reshape(PROF_KERNELS, PROF_BLOCKS, 16).astype(np.float64)
     print(f'# env-step kernel phases, {cfg_name} N={n}, {regime}, {steps} steps; '
@@ -93,6 +116,34 @@ def main():
         print(f'{name}: {top:.1f} us per wave (span {tot[14] * 0.01 / waves:.1f}), {waves / steps:.0f} waves per step')
         for (s, label), v in zip(marks, t):
             print(f'  {label:44s} {v:9.2f} us  {100 * v / max(top, 1e-9):5.1f}%')
+        if per_step:
+            waves_report(per_step, kid, base, marks)
+
+
+def waves_report(per_step, kid, base, marks):
+    """Span percentiles of the active waves of each step, and the phases of
+    the slowest 1 % of all waves against the mean of all."""
+    pct = []
+    rows = []
+    for r in per_step:
+        k = r[kid]
+        act = k[:, 15] > 0
+        if not act.any():
+            continue
+        sp = k[act, 14] * 0.01
+        pct.append(np.percentile(sp, [50, 90, 99, 100]))
+        rows.append(k[act])
+    if not pct:
+        return
+    pct = np.array(pct).mean(axis=0)
+    allw = np.concatenate(rows)
+    sp = allw[:, 14]
+    top = allw[sp >= np.percentile(sp, 99)]
+    print(f'  waves per step: span p50 {pct[0]:.1f}, p90 {pct[1]:.1f}, p99 {pct[2]:.1f}, max {pct[3]:.1f} us '
+          f'(mean over {len(per_step)} steps)')
+    print(f'  {"phase (us per wave)":44s} {"all":>9s} {"slowest 1%":>11s}')
+    for s, label in marks:
+        print(f'  {label:44s} {allw[:, s - base].mean() * 0.01:9.2f} {top[:, s - base].mean() * 0.01:11.2f}')
 
 
 if __name__ == '__main__':
