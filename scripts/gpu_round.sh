@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
-#   tests t:<files> ab regimes smoke bench benchq benchcw0 shards env full
+#   tests t:<files> testslib:<variant> ab regimes smoke bench benchq benchcw0 shards env full
 #   envprof2 prof profd envprof pmc pmcenv sqmix profenv profwaves split0ab slowkab
 #   libab:<variant> ktrace:<libs> ktraced:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
 #   polab[:<libs>] polpmc trend[:<iterations>])
@@ -17,6 +17,11 @@ for step in "$@"; do
     tests)
       cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread \
         -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { echo "tests failed"; exit 1; } ;;
+    testslib:*)
+      # testslib:<variant>: the GPU suite on masurvival/_lib/libmas_<variant>.so (MAS_LIB)
+      cd $R && MAS_LIB=$R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_${step#testslib:}.so timeout -k 10 900 \
+        python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > $O/gpu_tests_${step#testslib:}.log 2>&1 || { echo "tests failed"; exit 1; } ;;
     t:*)
       # t:<file.py>[,<file.py>...]: those GPU test files only
       F=$(echo ${step#t:} | tr ',' ' ' | sed 's#\([^ ]*\)#tests/\1#g')
