@@ -155,7 +155,12 @@ int mas_set_state(mas_handle* h, const void* src, void* stream);
  *   advantages/returns [T][n_columns] (out), adv_sums double[2] (out:
  *   sum and sum of squares of the advantages, for normalisation).
  *   delta_t = r_t + gamma * V_{t+1} * (1 - d_t) - V_t
- *   A_t     = delta_t + gamma * lambda * (1 - d_t) * A_{t+1}      */
+ *   A_t     = delta_t + gamma * lambda * (1 - d_t) * A_{t+1}
+ * The partial sums go through per-device slots in the library: calls on
+ * one device must not run concurrently (stream-ordered calls are fine).
+ * MAS_GAE_SCAN=1 (environment, read per call) selects the wavefront scan
+ * over time instead of the per-column walk; same results within fp32
+ * rounding.                                                            */
 int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards, const float* values,
             const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
             void* stream);

@@ -5,7 +5,7 @@ set -e
 C=$(dirname $0)/../gym-ma-survival-2d_amd/csrc
 cd $C
 L=../masurvival/_lib
-FLAGS="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -Wno-unused-result"
+FLAGS="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -Wno-unused-result -Wno-pass-failed -mllvm -pragma-unroll-threshold=200000"  # (the Makefile's)
 while [ $# -gt 0 ]; do
   n=$1; f=$2; shift 2
   mkdir -p build_pv

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
-#   tests t:<files> testslib:<variant> ab regimes smoke bench benchq benchcw0 shards env full
+#   tests t:<files> testslib:<variant> gaebench ab regimes smoke bench benchq benchcw0 shards env full
 #   envprof2 prof profd envprof pmc pmcenv sqmix profenv profwaves split0ab slowkab
 #   libab:<variant> ktrace:<libs> ktraced:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
 #   polab[:<libs>] polpmc trend[:<iterations>])
@@ -27,6 +27,15 @@ for step in "$@"; do
       F=$(echo ${step#t:} | tr ',' ' ' | sed 's#\([^ ]*\)#tests/\1#g')
       cd $R && timeout -k 10 900 python -u -m pytest $F -m gpu -x -v -s --timeout 300 --timeout-method thread \
         -p no:cacheprovider > $O/gpu_tests_sel.log 2>&1 || { echo "selected tests failed"; exit 1; } ;;
+    gaebench*)
+      # gaebench[:<variant>,...]: mas_gae timing on the default library, then on each variant (MAS_LIB)
+      cd $R && timeout -k 10 200 python -u scripts/gae_bench.py > $O/gae_bench.txt 2>&1 || exit 1
+      if [ "$step" != gaebench ]; then
+        for v in $(echo ${step#gaebench:} | tr ',' ' '); do
+          cd $R && MAS_LIB=$R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so timeout -k 10 200 python -u scripts/gae_bench.py \
+            >> $O/gae_bench.txt 2>&1 || exit 1
+        done
+      fi ;;
     ab)
       cd $R && timeout -k 10 600 python -u scripts/ab_solve_golden.py all > $O/ab_golden.log 2>&1 || { echo "A/B differs"; exit 1; } ;;
     regimes)

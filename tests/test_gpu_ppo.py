@@ -13,8 +13,13 @@ from masurvival.ppo import PPOConfig, PPOTrainer, gae, gae_reference  # noqa: E4
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 
 
-@pytest.mark.parametrize('T,N,A', [(64, 1000, 4), (13, 37, 2), (1, 5, 3), (64, 65536, 4)])
-def test_gae_kernel_matches_reference(T, N, A):
+@pytest.mark.parametrize('scan', ['0', '1'])
+@pytest.mark.parametrize('T,N,A', [(64, 1000, 4), (13, 37, 2), (1, 5, 3), (64, 65536, 4), (150, 300, 4)])
+def test_gae_kernel_matches_reference(T, N, A, scan, monkeypatch):
+    """Both forms of mas_gae: the per-column walk (default) and the
+    wavefront scan over time (MAS_GAE_SCAN=1; T = 150 spans three 64-step
+    chunks, so the carries between chunks are covered)."""
+    monkeypatch.setenv('MAS_GAE_SCAN', scan)
     g = torch.Generator(device='cuda').manual_seed(T * 1000 + N)
     r = torch.randn((T, N, A), device='cuda', generator=g)
     v = torch.randn((T + 1, N, A), device='cuda', generator=g)
