@@ -560,13 +560,17 @@ __device__ __forceinline__ void store_rows2(__bf16* base, int64_t M, int64_t row
     const uint32_t m2 = OFF32 ? __builtin_amdgcn_readfirstlane((uint32_t)(M * 2)) : 0u;
     const uint32_t lane_off = OFF32 ? ((uint32_t)((int)odd + 4 * h) * m2 + (uint32_t)(row & ~(int64_t)1) * 2u) : 0u;
     const u4 w[2] = {__builtin_bit_cast(u4, v[0]), __builtin_bit_cast(u4, v[1])};
+    // byte selectors of v_perm_b32 over {partner word, own word} (own bytes
+    // 0-3, partner's 4-7): even row: own feature 2j, then the partner's
+    // (row + 1); odd row: the partner's feature 2j + 1 (row - 1), then its own
+    const uint32_t psel = odd ? 0x03020706u : 0x05040100u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        // features 2j (low half) and 2j + 1 (high half) of this lane's row
-        const uint32_t a = w[j >> 2][j & 3] & 0xffffu, b = w[j >> 2][j & 3] >> 16;
-        // quad_perm [1, 0, 3, 2]: lane l reads lane l ^ 1
-        const uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? a : b), 0xB1, 0xF, 0xF, false) & 0xffffu;
-        const uint32_t word = odd ? (r | (b << 16)) : (a | (r << 16));
+        // features 2j (low half) and 2j + 1 (high half) of this lane's row;
+        // quad_perm [1, 0, 3, 2]: lane l reads lane l ^ 1's whole word
+        const uint32_t own = w[j >> 2][j & 3];
+        const uint32_t par = (uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0xB1, 0xF, 0xF, false);
+        const uint32_t word = __builtin_amdgcn_perm(par, own, psel);
         if (OFF32) {
             const uint32_t K = (uint32_t)(32 * mt + 2 * (j & 1) + 8 * (j >> 1));
             *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(base) + (lane_off + K * m2)) = word;
