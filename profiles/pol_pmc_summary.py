@@ -13,6 +13,8 @@ def main(d, out):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for sub in ('fetch', 'write', 'p1', 'p2'):
         path = os.path.join(d, sub, 'run_counter_collection.csv')
+        if not os.path.exists(path):  # (the gpu_round.sh step's directory names)
+            path = os.path.join(d, 'pol_' + sub, 'run_counter_collection.csv')
         if not os.path.exists(path):
             continue
         for r in csv.DictReader(open(path)):
