@@ -358,7 +358,7 @@ def main():
                                     if args.mode == 'ppo' else None}},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                     'kernel': 'mas_step launch group (k_pre_lanes, k_gen_solve_g, k_post_lanes with the auto-reset in place; the slow list'"'"'s pair on the side stream)' if args.shards == 1 else
+                     'kernel': 'mas_step launch group (k_pre_lanes, k_gen_solve_g, k_post_lanes with the auto-reset in place; the slow-list pair on the side stream)' if args.shards == 1 else
                      f'mas_step launch group of one shard ({args.shards} shards on concurrent streams)',
                      'kernel_ms': kern_ms, 'bytes_per_env_step': b_env,
                      'bytes_per_launch': b_env * n_launch},
