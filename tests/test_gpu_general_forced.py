@@ -26,8 +26,22 @@ from oracle import OracleEnv  # noqa: E402
 HI = np.array([3, 3, 3, 2, 2, 2])
 
 
+# the xxl class (8 agents, 20 heals, 16 randomized boxes: 20 statics per
+# agent, the widest general-path lane groups)
+XXL_FFA8 = {
+    'agents': {'n_agents': 8, 'agent_size': 1},
+    'spawn_grid': {'grid_size': 8, 'floor_size': 22},
+    'heals': {'reset_spawns': {'n_items': 20, 'item_size': 0.5}, 'heal': {'healing': 50}},
+    'boxes': {'reset_spawns': {'n_boxes': 16, 'box_size': 1}, 'ownership': False,
+              'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20,
+              'randomized_shape': {'avg_w': 1.0, 'std_w': 0.5, 'avg_h': 1.0, 'std_h': 0.5}},
+    'inventory': {'slots': 8},
+    'melee': {'range': 2, 'damage': 20, 'cooldown': 40, 'drift': True}}
+
+
 @pytest.mark.parametrize('name,cfg,n,T', [('C5 ffa4 shard', C5_CONFIG, 16384, 60),
-                                          ('C3 2v2', C3_CONFIG, 8192, 60)])
+                                          ('C3 2v2', C3_CONFIG, 8192, 60),
+                                          ('xxl ffa8', XXL_FFA8, 4096, 60)])
 def test_all_envs_on_general_path_match_oracle(name, cfg, n, T):
     rc = ResolvedConfig(cfg)
     try:
