@@ -120,6 +120,23 @@ def test_lidars_ffa4_batched_auto_reset_matches_oracle():
     assert resets > 0 and hits > 0, (resets, hits)
 
 
+LID_XXL = {
+    'agents': {'n_agents': 8, 'agent_size': 1},
+    'spawn_grid': {'grid_size': 8, 'floor_size': 22},
+    'heals': {'reset_spawns': {'n_items': 20, 'item_size': 0.5}, 'heal': {'healing': 50}},
+    'boxes': {'reset_spawns': {'n_boxes': 12, 'box_size': 1}, 'ownership': False,
+              'item': {'item_size': 0.5, 'offset': 0.75}, 'health': 20},
+    'inventory': {'slots': 6},
+    'melee': MELEE, 'safe_zone': SHORT_ZONE,
+    'lidars': {'n_lasers': 12, 'fov': 1.5 * math.pi, 'depth': 7}}
+
+
+def test_lidars_xxl_batched_auto_reset_matches_oracle():
+    """The xxl class (8 agents, 20 heals, 12 boxes), 12 lasers, 512 envs, 150 steps."""
+    resets, _, hits = _run(LID_XXL, 512, 150, 0, 44)
+    assert resets > 0 and hits > 0, (resets, hits)
+
+
 def test_lidars_masked_reset_matches_oracle():
     """mas_reset(mask) every 25 steps (launch_reset -> k_obs and k_lidar with the
     mask) between auto-reset steps: 2v2 8 lasers x1024."""
