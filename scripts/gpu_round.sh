@@ -98,9 +98,11 @@ for step in "$@"; do
         cd $R && MAS_SPLIT=$sp timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/split0ab_driver_sp$sp.json 2>> $O/split0ab.err || exit 1
         cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline >> $O/split0ab_env_sp$sp.json 2>> $O/split0ab.err || exit 1
       done ;;
-    slowkab)
-      # MAS_SLOW_K (TOI events of an env's step that send it to the slow list next step): 4 (default) vs 2 vs 1
-      for k in 4 2 1 4 2 1; do
+    slowkab*)
+      # MAS_SLOW_K (TOI events of an env's step that send it to the slow list next step), alternating:
+      # slowkab = 4 (default) vs 2 vs 1; slowkab:<k>,<k>,... those values
+      KS="4 2 1"; [ "$step" != slowkab ] && KS=$(echo ${step#slowkab:} | tr ',' ' ')
+      for k in $KS $KS; do
         cd $R && MAS_SLOW_K=$k timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/slowkab_driver_k$k.json 2>> $O/slowkab.err || exit 1
       done ;;
     libab:*)
