@@ -182,18 +182,39 @@ Poly4 poly_set4(const V2* in)
 // rewards, values and done flags land in LDS with coalesced row loads and the
 // advantages / returns leave the same way; each wave scans 16 of the columns.
 // The fp64 partial sums (sum adv, sum adv^2) feed the advantage
-// normalisation that the trainer all-reduces across ranks.
+// normalisation that the trainer all-reduces across ranks: each workgroup
+// stores its pair into its own slot of the caller's scratch (no atomics, no
+// library-global state, so concurrent calls on other streams are
+// independent and the sums are deterministic), and k_gae_sums adds the slots
+// in a fixed order.
 constexpr int kGaeCols = 64;  // columns per workgroup; time chunk = one wave's 64 lanes
-// the partial sums' slots (per device; zero between calls: k_gae_sums
-// re-zeroes them.  Calls on one device must not overlap -- the trainer's one
-// per update on its stream)
-constexpr int kGaeShards = 256;
-__device__ double g_gae_part[kGaeShards][2];
+constexpr int kGaeWalkCols = 256;  // columns per workgroup of k_gae_walk
+
+// a 256-thread workgroup's (s1, s2) into part[2 * blockIdx.x ..]: wave
+// butterflies, then the four waves in order (one plain store pair)
+__device__ __forceinline__ void gae_block_part(double s1, double s2, double* __restrict__ part)
+{
+    for (int off = 32; off > 0; off >>= 1) {
+        s1 += __shfl_xor(s1, off, 64);
+        s2 += __shfl_xor(s2, off, 64);
+    }
+    __shared__ double ws[4][2];
+    const int w = (int)(threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0) {
+        ws[w][0] = s1;
+        ws[w][1] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = ws[0][0] + ws[1][0] + ws[2][0] + ws[3][0];
+        part[2 * blockIdx.x + 1] = ws[0][1] + ws[1][1] + ws[2][1] + ws[3][1];
+    }
+}
 
 __global__ __launch_bounds__(256) void k_gae(int T, int64_t M, int A, const float* __restrict__ rew,
                                              const float* __restrict__ val, const uint8_t* __restrict__ done,
                                              float gamma, float lam, float* __restrict__ adv,
-                                             float* __restrict__ ret, double* __restrict__ sums)
+                                             float* __restrict__ ret, double* __restrict__ part)
 {
     __shared__ float sr[64][kGaeCols + 1];   // rewards, then the advantages
     __shared__ float sv[65][kGaeCols + 1];   // values (the chunk's and the next step's)
@@ -279,27 +300,11 @@ __global__ __launch_bounds__(256) void k_gae(int T, int64_t M, int A, const floa
         }
         __syncthreads();  // (the next chunk's loads reuse the tiles)
     }
-    // the workgroup's partial sums (wave butterflies, then its 4 waves), one
-    // atomic pair per workgroup into one of kGaeShards slots: a single
-    // address took every wave's atomic and serialised them (memory-side
-    // atomics on one address: ~20 ns each, 8192 of them were most of the
-    // old kernel's 161 us)
-    for (int off = 32; off > 0; off >>= 1) {
-        s1 += __shfl_xor(s1, off, 64);
-        s2 += __shfl_xor(s2, off, 64);
-    }
-    __shared__ double ws[4][2];
-    if (lane == 0) {
-        ws[w][0] = s1;
-        ws[w][1] = s2;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double* slot = g_gae_part[blockIdx.x % kGaeShards];
-        atomicAdd(&slot[0], ws[0][0] + ws[1][0] + ws[2][0] + ws[3][0]);
-        atomicAdd(&slot[1], ws[0][1] + ws[1][1] + ws[2][1] + ws[3][1]);
-    }
-    (void)sums;
+    // the workgroup's partial sums (wave butterflies, then its 4 waves) into
+    // its own slot of the caller's scratch (round 4's one-address atomics
+    // serialised, ~20 ns each; round 5's 256 shared slots made concurrent
+    // calls race: DESIGN.md 4.3.10)
+    gae_block_part(s1, s2, part);
 }
 
 // The default form: one thread per column walking t = T-1..0, every
@@ -311,7 +316,7 @@ constexpr int kGaeChunk = 8;
 __global__ __launch_bounds__(256) void k_gae_walk(int T, int64_t M, int A, const float* __restrict__ rew,
                                              const float* __restrict__ val, const uint8_t* __restrict__ done,
                                              float gamma, float lam, float* __restrict__ adv,
-                                             float* __restrict__ ret, double* __restrict__ sums)
+                                             float* __restrict__ ret, double* __restrict__ part)
 {
     const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t E = M / A;
@@ -354,51 +359,34 @@ __global__ __launch_bounds__(256) void k_gae_walk(int T, int64_t M, int A, const
             vnext = v;
         }
     }
-    // the workgroup's partial sums into one of the shard slots (k_gae)
+    // the workgroup's partial sums into its slot (k_gae)
+    gae_block_part(s1, s2, part);
+}
+
+// the slots' sum into adv_sums (fixed order: thread k adds slots k, k + 256,
+// ..., then a butterfly and the four waves in order)
+__global__ __launch_bounds__(256) void k_gae_sums(const double* __restrict__ part, int nblocks,
+                                                  double* __restrict__ sums)
+{
+    const int k = (int)threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+    for (int b = k; b < nblocks; b += 256) {
+        s1 += part[2 * b];
+        s2 += part[2 * b + 1];
+    }
     for (int off = 32; off > 0; off >>= 1) {
         s1 += __shfl_xor(s1, off, 64);
         s2 += __shfl_xor(s2, off, 64);
     }
     __shared__ double ws[4][2];
-    const int w = (int)(threadIdx.x >> 6);
-    if ((threadIdx.x & 63) == 0) {
-        ws[w][0] = s1;
-        ws[w][1] = s2;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double* slot = g_gae_part[blockIdx.x % kGaeShards];
-        atomicAdd(&slot[0], ws[0][0] + ws[1][0] + ws[2][0] + ws[3][0]);
-        atomicAdd(&slot[1], ws[0][1] + ws[1][1] + ws[2][1] + ws[3][1]);
-    }
-    (void)sums;
-}
-
-// the shards' sum into adv_sums, and the shards zeroed for the next call
-__global__ __launch_bounds__(kGaeShards) void k_gae_sums(double* __restrict__ sums)
-{
-    const int k = (int)threadIdx.x;
-    double s1 = g_gae_part[k][0], s2 = g_gae_part[k][1];
-    g_gae_part[k][0] = 0.0;
-    g_gae_part[k][1] = 0.0;
-    for (int off = 32; off > 0; off >>= 1) {
-        s1 += __shfl_xor(s1, off, 64);
-        s2 += __shfl_xor(s2, off, 64);
-    }
-    __shared__ double ws[kGaeShards / 64][2];
     if ((k & 63) == 0) {
         ws[k >> 6][0] = s1;
         ws[k >> 6][1] = s2;
     }
     __syncthreads();
     if (k == 0) {
-        double t1 = 0.0, t2 = 0.0;
-        for (int q = 0; q < kGaeShards / 64; ++q) {
-            t1 += ws[q][0];
-            t2 += ws[q][1];
-        }
-        sums[0] = t1;
-        sums[1] = t2;
+        sums[0] = ws[0][0] + ws[1][0] + ws[2][0] + ws[3][0];
+        sums[1] = ws[0][1] + ws[1][1] + ws[2][1] + ws[3][1];
     }
 }
 
@@ -902,9 +890,14 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing((hipStream_t)stream, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
-    // a captured step appends nothing to the slow list (slow_route 0): its
-    // k_pre zeroes the slot mas_debug_counters reads after it, on every replay
-    if (capturing) P.slow_prev = P.slow_count;
+    // a captured step appends nothing to the slow list (slow_route 0).  Its
+    // k_pre zeroes BOTH count slots on every replay: the host's slot parity
+    // flips once at capture time but not per replay, so the eager step after
+    // the replays may take either slot, and the slot it takes must not hold
+    // the count of the last eager step before the capture (its
+    // side stream would re-run those stale entries beside the main stream).
+    // mas_debug_counters then reads 0 for the captured step, whichever slot.
+    P.slow_zero2 = capturing ? P.slow_count : nullptr;
     // the slow split runs while the general kernels keep flagging slow envs
     // (the signal lags the device by the steps in flight: slow envs persist
     // for many steps); without any, no slow chain
@@ -983,28 +976,36 @@ int mas_set_state(mas_handle* h, const void* src, void* stream)
     return MAS_OK;
 }
 
+int64_t mas_gae_scratch_doubles(int64_t n_columns)
+{
+    return n_columns > 0 ? 2 * ((n_columns + kGaeCols - 1) / kGaeCols) : -1;
+}
+
 int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards, const float* values,
             const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
-            void* stream)
+            double* scratch, void* stream)
 {
     if (T <= 0 || n_columns <= 0 || n_agents <= 0 || n_columns % n_agents)
         return fail(MAS_ERR_INVALID_ARG, "mas_gae: need T > 0 and n_columns a positive multiple of n_agents");
-    if (!rewards || !values || !done || !advantages || !returns || !adv_sums)
+    if (!rewards || !values || !done || !advantages || !returns || !adv_sums || !scratch)
         return fail(MAS_ERR_INVALID_ARG, "mas_gae: null argument");
+    if ((n_columns + kGaeCols - 1) / kGaeCols > 0x7fffffff)
+        return fail(MAS_ERR_INVALID_ARG, "mas_gae: n_columns too large");
     hipStream_t s = (hipStream_t)stream;
     // the per-column walk (default); MAS_GAE_SCAN=1: the wavefront scan over
     // time (measured 135 vs 61.5 us at T = 64, 65536 x 4 columns)
     const char* scan_env = getenv("MAS_GAE_SCAN");
+    int nblocks;
     if (scan_env && scan_env[0] == '1') {
-        dim3 g((unsigned)((n_columns + kGaeCols - 1) / kGaeCols));
-        hipLaunchKernelGGL(k_gae, g, dim3(256), 0, s, (int)T, (int64_t)n_columns, (int)n_agents, rewards, values,
-                           done, gamma, lam, advantages, returns, adv_sums);
+        nblocks = (int)((n_columns + kGaeCols - 1) / kGaeCols);
+        hipLaunchKernelGGL(k_gae, dim3((unsigned)nblocks), dim3(256), 0, s, (int)T, (int64_t)n_columns, (int)n_agents,
+                           rewards, values, done, gamma, lam, advantages, returns, scratch);
     } else {
-        dim3 g((unsigned)((n_columns + 255) / 256));
-        hipLaunchKernelGGL(k_gae_walk, g, dim3(256), 0, s, (int)T, (int64_t)n_columns, (int)n_agents, rewards,
-                           values, done, gamma, lam, advantages, returns, adv_sums);
+        nblocks = (int)((n_columns + kGaeWalkCols - 1) / kGaeWalkCols);
+        hipLaunchKernelGGL(k_gae_walk, dim3((unsigned)nblocks), dim3(256), 0, s, (int)T, (int64_t)n_columns,
+                           (int)n_agents, rewards, values, done, gamma, lam, advantages, returns, scratch);
     }
-    hipLaunchKernelGGL(k_gae_sums, dim3(1), dim3(kGaeShards), 0, s, adv_sums);
+    hipLaunchKernelGGL(k_gae_sums, dim3(1), dim3(256), 0, s, (const double*)scratch, nblocks, adv_sums);
     HIP_TRY(hipGetLastError());
     return MAS_OK;
 }

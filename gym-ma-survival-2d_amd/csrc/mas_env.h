@@ -116,6 +116,8 @@ struct Params {
     int* slow_count;     // its count slot this step: two slots alternate per split step (the split is
                          // decided on the host per mas_step, so it is never graph-captured)
     int* slow_prev;      // the other slot: k_pre zeroes it
+    int* slow_zero2;     // non-null in a graph-captured step: k_pre zeroes this slot too (both slots), so the
+                         // eager step after the replays appends to an empty slot whichever it takes
     uint8_t* slow_flag;  // [N] set by k_gen_solve_g, read and cleared by k_pre (cleared by resets)
     int slow_k;          // 0: no slow flags
     int slow_route;      // this step routes the flagged envs to the slow list (the slow split is on)
@@ -152,8 +154,9 @@ struct StepSplit {
 // atomics sat inside the timed phases.  Marks sit only at wave-convergent
 // points.  Phase slots: 0-5, 7 / 8-13 the general path's world steps 1 / 2
 // (kid 0; the slow list's, gen_sparse, kid 4); 20-25 k_pre_lanes (kid 1);
-// 41-45 k_post_lanes (kid 2; over a list, kid 5); 37-40 k_obs (kid 3).
-constexpr int kProfHead = 64, kProfKernels = 6, kProfBlocks = 16384;
+// 41-45 k_post_lanes (kid 2; over a list, kid 5); 37-40 k_obs (kid 3; over a
+// list, kid 6).
+constexpr int kProfHead = 64, kProfKernels = 7, kProfBlocks = 16384;
 constexpr int kProfWords = kProfHead + kProfKernels * kProfBlocks * 16;  // 8-B words of P.prof
 #ifdef MAS_PROFILE
 constexpr int kProfSlots = 48;

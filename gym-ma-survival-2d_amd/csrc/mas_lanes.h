@@ -436,6 +436,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
     // previous step's first post kernel
     if (blockIdx.x == 0 && lane == 0) {
         *P.slow_prev = 0;
+        if (P.slow_zero2) *P.slow_zero2 = 0;
         P.reset_count[0] = 0;  // the auto-reset lists of this step (main and side stream)
         P.reset_count[1] = 0;
     }

@@ -1209,7 +1209,14 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
 #endif
     };
     const int64_t b0 = blockIdx.x;
-    if (b0 < nblk) copy_db(buf(0), F + Lo.w1(), (KS < kKc ? KS : kKc) * kMT * 64);  // prologue
+    // the prologue's copies land before the loop (the same order as landing
+    // them in the first block's phase A), so the loop's phase-A wait is always
+    // the counted one: no path reaches it with fewer VMEM ops after the
+    // copies than it counts (scripts/check_policy_waits.py checks every path)
+    if (b0 < nblk) {
+        copy_db(buf(0), F + Lo.w1(), (KS < kKc ? KS : kKc) * kMT * 64);
+        land_db<0>();
+    }
     for (int64_t blk = b0; blk < nblk; blk += gridDim.x) {
         // the lane index made opaque per block: keeps the compiler from
         // hoisting the blocks' LDS and store addresses out of the loop (held
@@ -1231,8 +1238,7 @@ __global__ __launch_bounds__(64 * kDW, 1) void k_policy_train_db(TrainArgs A, in
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
                 if (c == 0) {
-                    if (blk == b0) land_db<0>();   // the prologue's copies
-                    else land_db<32>();            // phase G: 32 dA1 stores after them
+                    if (blk != b0) land_db<32>();  // phase G: 32 dA1 stores after them
                 } else {
                     if (c == 1) land_db<KS>();  // chunk 0: the x loads after them
                     else land_db<0>();

@@ -61,7 +61,8 @@ SIGNATURES = {
     'mas_get_state': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'mas_set_state': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'mas_gae': (c_int32, [c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
-                          c_void_p, c_void_p, c_void_p, c_void_p]),
+                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'mas_gae_scratch_doubles': (c_int64, [c_int64]),
     'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_debug_guards': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_debug_force_general': (c_int32, [c_void_p, c_int32]),

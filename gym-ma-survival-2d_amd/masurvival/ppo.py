@@ -172,8 +172,16 @@ def evaluate_actions(logits, actions):
     return logp, ent
 
 
-def gae(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents, stream=None):
-    """HIP GAE over [T, N*A] columns (include/masurvival.h mas_gae)."""
+def gae_scratch(n_columns, device):
+    """The partial-sum scratch one mas_gae call needs (mas_gae_scratch_doubles)."""
+    n = load_library().mas_gae_scratch_doubles(int(n_columns))
+    return torch.empty((n,), device=device, dtype=torch.float64)
+
+
+def gae(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents, stream=None, scratch=None):
+    """HIP GAE over [T, N*A] columns (include/masurvival.h mas_gae).  scratch:
+    float64 device tensor of mas_gae_scratch_doubles(N*A) (allocated here when
+    None); concurrent calls need their own scratch and outputs."""
     lib = load_library()
     T = rewards.shape[0]
     M = rewards[0].numel()
@@ -181,11 +189,15 @@ def gae(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents
         assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
     assert values.shape[0] == T + 1 and dones.shape[0] == T and dones.dtype == torch.uint8
     assert dones[0].numel() * n_agents == M and sums_out.dtype == torch.float64
+    if scratch is None:
+        scratch = gae_scratch(M, rewards.device)
+    assert scratch.is_cuda and scratch.dtype == torch.float64 and scratch.numel() >= lib.mas_gae_scratch_doubles(M)
     s = stream if stream is not None else torch.cuda.current_stream(rewards.device).cuda_stream
     check(lib.mas_gae(T, M, n_agents, ctypes.c_void_p(rewards.data_ptr()), ctypes.c_void_p(values.data_ptr()),
                       ctypes.c_void_p(dones.data_ptr()), float(gamma), float(lam),
                       ctypes.c_void_p(adv_out.data_ptr()), ctypes.c_void_p(ret_out.data_ptr()),
-                      ctypes.c_void_p(sums_out.data_ptr()), ctypes.c_void_p(s)))
+                      ctypes.c_void_p(sums_out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                      ctypes.c_void_p(s)))
 
 
 def gae_reference(rewards, values, dones, gamma, lam, n_agents):
@@ -203,7 +215,8 @@ def gae_reference(rewards, values, dones, gamma, lam, n_agents):
     return adv.reshape(rewards.shape), (adv + v[:T]).reshape(rewards.shape)
 
 
-def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents, stream=None):
+def gae_reference_into(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents, stream=None,
+                       scratch=None):
     """Same contract as gae() on host tensors -- test double for the CPU
     multi-process tests only (the product trainer always runs the HIP kernel)."""
     adv, ret = gae_reference(rewards, values, dones, gamma, lam, n_agents)
@@ -526,6 +539,7 @@ class RolloutBuffer:
         self.adv = torch.zeros((T, N, A), **f)
         self.ret = torch.zeros((T, N, A), **f)
         self.adv_sums = torch.zeros((2,), device=device, dtype=torch.float64)
+        self.gae_scratch = None  # mas_gae's partial sums (made at the first HIP GAE call)
         self.xb = None  # fused path: bf16 policy-input rows [T, N*A, Dp] written by mas_policy_act
 
 
@@ -656,7 +670,10 @@ class PPOTrainer:
         else:
             _, v = self._fwd(b.obs[c.horizon])
             b.values[c.horizon].copy_(v)
-        self.gae_impl(b.rewards, b.values, b.dones, c.gamma, c.lam, b.adv, b.ret, b.adv_sums, self.env.n_agents)
+        if self.gae_impl is gae and b.gae_scratch is None:
+            b.gae_scratch = gae_scratch(b.N * b.A, self.device)
+        self.gae_impl(b.rewards, b.values, b.dones, c.gamma, c.lam, b.adv, b.ret, b.adv_sums, self.env.n_agents,
+                      scratch=b.gae_scratch)
         stats = torch.cat([b.adv_sums, torch.tensor([float(b.adv.numel())], device=self.device,
                                                      dtype=torch.float64)])
         if self.collectives:

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define MAS_ABI_VERSION 1
+#define MAS_ABI_VERSION 2  /* 2: mas_gae takes the caller's partial-sum scratch */
 
 #define MAS_OK 0
 #define MAS_ERR_INVALID_ARG (-1)
@@ -156,14 +156,19 @@ int mas_set_state(mas_handle* h, const void* src, void* stream);
  *   sum and sum of squares of the advantages, for normalisation).
  *   delta_t = r_t + gamma * V_{t+1} * (1 - d_t) - V_t
  *   A_t     = delta_t + gamma * lambda * (1 - d_t) * A_{t+1}
- * The partial sums go through per-device slots in the library: calls on
- * one device must not run concurrently (stream-ordered calls are fine).
+ * scratch: DEVICE double[mas_gae_scratch_doubles(n_columns)], the call's
+ * per-workgroup partial sums (no initialisation needed; the library keeps
+ * no state between calls, so calls on different streams -- or handles,
+ * trainers, threads -- may run concurrently as long as each has its own
+ * scratch and outputs).  adv_sums is summed in a fixed order: the same
+ * inputs give the same bits.
  * MAS_GAE_SCAN=1 (environment, read per call) selects the wavefront scan
  * over time instead of the per-column walk; same results within fp32
  * rounding.                                                            */
+int64_t mas_gae_scratch_doubles(int64_t n_columns);
 int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards, const float* values,
             const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
-            void* stream);
+            double* scratch, void* stream);
 
 /* Rollout side: sample the six action heads (MultiDiscrete [3,3,3,2,2,2]) of
  * n_rows agent rows from logits [n_rows][row_stride] (first 15 floats of a

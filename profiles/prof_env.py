@@ -24,7 +24,7 @@ import torch  # noqa: E402
 
 from masurvival import abi  # noqa: E402
 
-PROF_HEAD, PROF_KERNELS, PROF_BLOCKS = 64, 6, 16384  # mas_env.h kProfHead / kProfKernels / kProfBlocks
+PROF_HEAD, PROF_KERNELS, PROF_BLOCKS = 64, 7, 16384  # mas_env.h kProfHead / kProfKernels / kProfBlocks
 PROF_WORDS = PROF_HEAD + PROF_KERNELS * PROF_BLOCKS * 16
 GEN = [(0, 'ws1 load'), (1, 'ws1 collide'), (2, 'ws1 island solve'), (5, 'ws1 body shuffles + impulse-store fence'),
        (3, 'ws1 SolveTOI'), (4, 'ws1 stores'), (7, 'fence: ws1 stores complete'), (8, 'ws2 load'),
@@ -42,6 +42,8 @@ KERNELS = [
     ('k_post_lanes (all / main envs)', 2, 41, POST),
     ('k_post_lanes (slow list, side stream)', 5, 41, POST),
     ('k_obs', 3, 37, [(37, 'auto-reset'), (38, 'state load'), (39, 'row writer (windows)'), (40, 'tile stores')]),
+    ('k_obs (over a list)', 6, 37, [(37, 'auto-reset'), (38, 'state load'), (39, 'row writer (windows)'),
+                                    (40, 'tile stores')]),
 ]
 
 

@@ -5,7 +5,7 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'gym-ma-survival-2d_amd'))
 import torch  # noqa: E402
 
-from masurvival.ppo import gae  # noqa: E402
+from masurvival.ppo import gae, gae_scratch  # noqa: E402
 
 T, N, A = 64, 65536, 4
 g = torch.Generator(device='cuda').manual_seed(0)
@@ -14,13 +14,14 @@ v = torch.randn((T + 1, N, A), device='cuda', generator=g)
 d = (torch.rand((T, N), device='cuda', generator=g) < 0.05).to(torch.uint8)
 adv, ret = torch.empty_like(r), torch.empty_like(r)
 sums = torch.empty(2, device='cuda', dtype=torch.float64)
+sc = gae_scratch(N * A, 'cuda')
 for _ in range(3):
-    gae(r, v, d, 0.99, 0.95, adv, ret, sums, A)
+    gae(r, v, d, 0.99, 0.95, adv, ret, sums, A, scratch=sc)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for _ in range(20):
-    gae(r, v, d, 0.99, 0.95, adv, ret, sums, A)
+    gae(r, v, d, 0.99, 0.95, adv, ret, sums, A, scratch=sc)
 e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) * 1000 / 20

@@ -116,6 +116,21 @@ def test_captured_step_of_split_handle_replays_like_eager(monkeypatch):
         general += c1
     assert general > 0
     assert torch.equal(eager.get_state(), graph.get_state())
+    # eager steps on the split handle after the replays:
+    # the replays flagged slow envs, so the split turns on again and its first
+    # step appends to a slow-list count slot the captured k_pre must have
+    # zeroed (the host's slot parity did not move during the replays)
+    side = 0
+    for t in range(40):
+        a = (torch.rand((n, graph.n_agents, 6), generator=gen, device=graph.device) * hi).to(torch.int8)
+        o1, r1, d1, _ = eager.step(a)
+        o2, r2, d2, _ = graph.step(a)
+        assert torch.equal(d1, d2), (name, 'after replays', t)
+        assert torch.equal(r1, r2), (name, 'after replays', t)
+        assert torch.equal(o1, o2), (name, 'after replays', t)
+        side += int((graph.gen_flags() == 2).sum())
+    assert side > 0, name  # the slow list ran again after the replays
+    assert torch.equal(eager.get_state(), graph.get_state())
     assert eager.debug_guards()['list_overflow'] == 0
     assert graph.debug_guards()['list_overflow'] == 0
     del g

@@ -35,6 +35,41 @@ def test_gae_kernel_matches_reference(T, N, A, scan, monkeypatch):
     assert np.isclose(float(sums[1]), float((adv.double() ** 2).sum()), rtol=1e-9)
 
 
+@pytest.mark.parametrize('scan', ['0', '1'])
+def test_gae_concurrent_calls_on_two_streams(scan, monkeypatch):
+    """Two mas_gae calls in flight at once on two streams, each with its own
+    scratch and outputs, both checked against the torch restatement; the
+    sums are also bit-stable from call to call (fixed summation order)."""
+    monkeypatch.setenv('MAS_GAE_SCAN', scan)
+    from masurvival.ppo import gae_scratch
+    T, N, A = 64, 65536, 4
+    cases = []
+    for k in range(2):
+        g = torch.Generator(device='cuda').manual_seed(77 + k)
+        r = torch.randn((T, N, A), device='cuda', generator=g)
+        v = torch.randn((T + 1, N, A), device='cuda', generator=g)
+        d = (torch.rand((T, N), device='cuda', generator=g) < 0.05).to(torch.uint8)
+        cases.append(dict(r=r, v=v, d=d, adv=torch.empty_like(r), ret=torch.empty_like(r),
+                          sums=torch.empty(2, device='cuda', dtype=torch.float64),
+                          scratch=gae_scratch(N * A, 'cuda'), stream=torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for c in cases:  # interleaved launches: both streams' kernels overlap
+            gae(c['r'], c['v'], c['d'], 0.99, 0.95, c['adv'], c['ret'], c['sums'], A,
+                stream=c['stream'].cuda_stream, scratch=c['scratch'])
+        torch.cuda.synchronize()
+        for c in cases:
+            ra, rr = gae_reference(c['r'], c['v'], c['d'], 0.99, 0.95, A)
+            torch.testing.assert_close(c['adv'], ra, atol=1e-5, rtol=1e-5)
+            torch.testing.assert_close(c['ret'], rr, atol=1e-5, rtol=1e-5)
+            assert np.isclose(float(c['sums'][0]), float(c['adv'].double().sum()), rtol=1e-9, atol=1e-6)
+            assert np.isclose(float(c['sums'][1]), float((c['adv'].double() ** 2).sum()), rtol=1e-9)
+            if rep == 0:
+                c['first'] = c['sums'].clone()
+            else:
+                assert torch.equal(c['sums'], c['first'])
+
+
 def test_ppo_iteration_on_env():
     env = VecMaSurvival(C3_CONFIG, n_envs=512, auto_reset=True)
     tr = PPOTrainer(env, PPOConfig(horizon=16), seed=0)
