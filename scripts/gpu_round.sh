@@ -2,7 +2,7 @@
 # One GPU measurement pass (run via gpurun from the repo root):
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
 #   tests t:<files> testslib:<variant> gaebench ab regimes smoke bench benchq benchcw0 shards env full
-#   envprof2 prof profd envprof pmc pmcenv sqmix profenv profwaves split0ab slowkab
+#   c4rank envprof2 prof profd envprof pmc pmcenv sqmix profenv profwaves split0ab slowkab
 #   libab:<variant> ktrace:<libs> ktraced:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
 #   polab[:<libs>] polpmc trend[:<iterations>])
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
@@ -22,6 +22,11 @@ for step in "$@"; do
       cd $R && MAS_LIB=$R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_${step#testslib:}.so timeout -k 10 900 \
         python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
         > $O/gpu_tests_${step#testslib:}.log 2>&1 || { echo "tests failed"; exit 1; } ;;
+    testsv:*)
+      # testsv:<variant>: the GPU suite on a narrowed variant library (MAS_CLASSES="2v2 ffa": other classes skip)
+      cd $R && MAS_CLASSES="2v2 ffa" MAS_LIB=$R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_${step#testsv:}.so timeout -k 10 900 \
+        python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > $O/gpu_tests_${step#testsv:}.log 2>&1 || { echo "tests failed"; exit 1; } ;;
     t:*)
       # t:<file.py>[,<file.py>...]: those GPU test files only
       F=$(echo ${step#t:} | tr ',' ' ' | sed 's#\([^ ]*\)#tests/\1#g')
@@ -63,6 +68,17 @@ for step in "$@"; do
       # the C4 / C5 workloads at their configured env counts on one GPU
       cd $R && timeout -k 10 300 python bench.py --mode env --envs 262144 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_env_c4full.log 2>&1 || exit $?
       cd $R && timeout -k 10 300 python bench.py --mode env --config ffa4 --envs 131072 --steps 30 --warmup 10 --no-cpu-baseline > $O/bench_env_c5full.log 2>&1 || exit $? ;;
+    c4rank)
+      # the C4 per-rank workload of the 8-GPU target (2v2 x 262144 over 8 GPUs = 32768 per rank) in the
+      # driver-shaped PPO window: bench line, kernel trace, FETCH / WRITE passes
+      cd $R && timeout -k 10 300 python bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_c4rank.log 2>&1 || exit $?
+      cd $R && timeout -k 10 300 python bench.py --envs 32768 --no-cpu-baseline > $O/bench_c4rank.log 2>&1 || exit $?
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4rank -o run -- \
+        python3 $R/bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_c4rank.log 2>&1 || exit $?
+      for c in FETCH_SIZE WRITE_SIZE; do
+        cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "mas::k_" --output-format csv \
+          -d $O/pmc_${c}_c4rank -o run -- python3 $R/bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_${c}_c4rank.log 2>&1 || exit $?
+      done ;;
     envprof2)
       cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_env -o run -- \
         python3 $R/bench.py --mode env --no-cpu-baseline > $O/prof_env.log 2>&1 || exit $? ;;
@@ -113,6 +129,28 @@ for step in "$@"; do
           L=""; [ $lib != default ] && L="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$lib.so"
           cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $L >> $O/libab_driver_$lib.json 2>> $O/libab.err || exit 1
           cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline $L >> $O/libab_env_$lib.json 2>> $O/libab.err || exit 1
+        done
+      done ;;
+    varab:*)
+      # varab:<lib>:<VAR>:<v1>,<v2>,...: one library (main = libmas.so), the environment variable VAR at
+      # each value, alternating, twice: driver window, env-only 2v2 and FFA4 x16384
+      IFS=: read -r _ V VAR VALS <<< "$step"
+      LIB=""; [ "$V" != main ] && LIB="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$V.so"
+      for k in 1 2; do
+        for val in $(echo $VALS | tr ',' ' '); do
+          cd $R && env $VAR=$val timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $LIB >> $O/varab_${V}_driver_$VAR$val.json 2>> $O/varab.err || exit 1
+          cd $R && env $VAR=$val timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline $LIB >> $O/varab_${V}_env_$VAR$val.json 2>> $O/varab.err || exit 1
+          cd $R && env $VAR=$val timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline $LIB >> $O/varab_${V}_ffa_$VAR$val.json 2>> $O/varab.err || exit 1
+        done
+      done ;;
+    libabx:*)
+      # libabx:<lib>,<lib>,...: driver window, env-only 2v2 and FFA4 x16384 per library (main = libmas.so), alternating, twice
+      for k in 1 2; do
+        for v in $(echo ${step#libabx:} | tr ',' ' '); do
+          LIB=""; [ "$v" != main ] && LIB="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
+          cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $LIB >> $O/libabx_driver_$v.json 2>> $O/libabx.err || exit 1
+          cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline $LIB >> $O/libabx_env_$v.json 2>> $O/libabx.err || exit 1
+          cd $R && timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline $LIB >> $O/libabx_ffa_$v.json 2>> $O/libabx.err || exit 1
         done
       done ;;
     pmcenv)
