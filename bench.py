@@ -115,6 +115,61 @@ def cpu_baseline(config, leg_s=6.0, all_cores=False):
     return out
 
 
+def live_traffic(args, n, timeout_s=240):
+    """HBM traffic per mas_step of this same workload, measured now: two
+    child runs of this bench (same arguments, so the same seeds, regime and
+    timed window) under `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
+    (separate passes: the two do not fit one, MI355X_MICROARCH.md), summed
+    over the env-step kernels of each of the timed window's steps
+    (profiles/pmc_traffic.py).  The children end with one mas_flush_stats
+    (k_stats: 19 state words per env loaded and stored, 19 floats per env
+    written -- 4-B lanes, the access width of the env kernels' state words)
+    whose counters against those known bytes calibrate the raw counters for
+    this access width (the guide calibrates 16-B lanes only).  Child
+    processes, started after this run's timed region; returns a dict, or one
+    with 'error' when rocprofv3 is missing or a pass fails."""
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, 'profiles'))
+    import pmc_traffic
+    prof = shutil.which('rocprofv3')
+    if not prof:
+        return {'error': 'rocprofv3 not found'}
+    child = [a for a in sys.argv[1:] if a not in ('--cpu-all-cores',)]
+    child += ['--no-cpu-baseline', '--no-live-traffic', '--flush-stats']
+    if not any(a.startswith('--horizon') for a in child):
+        child += ['--horizon', str(args.horizon)]
+    out, t0 = {}, time.perf_counter()
+    with tempfile.TemporaryDirectory(prefix='mas_pmc_') as d:
+        for c in ('FETCH_SIZE', 'WRITE_SIZE'):
+            cmd = [prof, '--pmc', c, '--kernel-include-regex', 'mas::k_|k_stats', '--output-format', 'csv',
+                   '-d', os.path.join(d, c), '-o', 'run', '--', sys.executable, os.path.abspath(__file__)] + child
+            try:
+                r = subprocess.run(cmd, cwd=d, capture_output=True, text=True, timeout=timeout_s,
+                                   env=dict(os.environ, MAS_BENCH_CHILD='1'))
+            except subprocess.TimeoutExpired:
+                return {'error': f'{c} pass timed out after {timeout_s} s'}
+            csvs = [os.path.join(dp, f) for dp, _, fs in os.walk(os.path.join(d, c)) for f in fs
+                    if f.endswith('counter_collection.csv')]
+            if r.returncode != 0 or not csvs:
+                return {'error': f'{c} pass failed (rc {r.returncode}): ' + (r.stderr or '')[-300:]}
+            out[c] = csvs[0]
+        f, nf = pmc_traffic.per_step(out['FETCH_SIZE'], 'FETCH_SIZE', args.steps)
+        w, nw = pmc_traffic.per_step(out['WRITE_SIZE'], 'WRITE_SIZE', args.steps)
+        cal = {c: pmc_traffic.kernel_bytes(out[c], c, 'k_stats') for c in out}
+    fetch, write = sum(f.values()), sum(w.values())
+    known = 19 * 4 * n  # k_stats: 19 words per env loaded (fetch); 19 stored + 19 floats written (write)
+    res = {'fetch_bytes_per_step': fetch, 'write_bytes_per_step': write, 'traffic_bytes_per_step': fetch + write,
+           'steps_profiled': min(nf, nw), 'per_kernel_fetch': dict(f), 'per_kernel_write': dict(w),
+           'seconds': round(time.perf_counter() - t0, 1)}
+    if cal.get('FETCH_SIZE') and cal.get('WRITE_SIZE'):
+        kf, kw = cal['FETCH_SIZE'] / known, cal['WRITE_SIZE'] / (2 * known)
+        res['calibration'] = {'kernel': 'k_stats (mas_flush_stats), 4-B lanes', 'fetch_counted_over_known': kf,
+                              'write_counted_over_known': kw}
+        res['traffic_bytes_per_step_calibrated'] = fetch / kf + write / kw
+    return res
+
+
 def free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
@@ -146,17 +201,23 @@ def parse_args():
     ap.add_argument('--steps', type=int, default=128, help='timed rollout steps')
     ap.add_argument('--warmup', type=int, default=16)
     ap.add_argument('--preroll', type=int, default=None,
-                    help='untimed PPO iterations (ppo mode, default 2) or env steps (env mode, default 128) '
-                         'before the warmup')
+                    help='untimed PPO iterations (ppo mode, default: enough for >= 128 steps, at least 2) or env '
+                         'steps (env mode, default 128) before the warmup')
     ap.add_argument('--config', default='2v2')
     ap.add_argument('--envs', type=int, default=None, help='envs per GPU (default 65536 for 2v2)')
     ap.add_argument('--mode', choices=['ppo', 'env'], default='ppo',
                     help='ppo: policy forward + env step + buffer, GAE + PPO update every horizon; env: random actions')
-    ap.add_argument('--horizon', type=int, default=64)
+    ap.add_argument('--horizon', type=int, default=None,
+                    help='PPO rollout horizon; default: --steps when it is at most 64 (the timed window is then '
+                         'exactly one PPO iteration), else 64')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-all-cores', action='store_true',
                     help='add the CPU-baseline leg on every CPU this process may use (cpu_baseline leg iv)')
     ap.add_argument('--lib', default=None, help='alternative libmas*.so (A/B variants)')
+    ap.add_argument('--no-live-traffic', action='store_true',
+                    help='skip the two rocprofv3 PMC child runs that measure roofline.traffic (live_traffic)')
+    ap.add_argument('--flush-stats', action='store_true',
+                    help='end with one mas_flush_stats (the PMC child runs: the counters\' calibration kernel)')
     ap.add_argument('--shards', type=int, default=1,
                     help='env handles per GPU, each on its own HIP stream (vec_env.ShardedVecMaSurvival)')
     return ap.parse_args()
@@ -250,6 +311,13 @@ def main():
         env.step = timed(env.step)
 
     rev, uev = [], []  # whole rollout step / whole GAE + update, on the current stream
+    # the horizon: the timed window holds whole PPO iterations when it can
+    # (--steps <= 64: one iteration of exactly --steps rollout steps and its
+    # GAE + update), so ms_per_step is the training loop's steady-state cost
+    # per step; a window shorter than the horizon would carry a whole update
+    # of horizon steps' rows for fewer rollout steps
+    if args.horizon is None:
+        args.horizon = args.steps if args.steps <= 64 else 64
     if args.mode == 'ppo':
         from masurvival.ppo import PPOConfig, PPOTrainer
         pcfg = PPOConfig(horizon=args.horizon)
@@ -273,7 +341,9 @@ def main():
                 uev.append((u0, u1))
                 state['t'] = 0
                 state['updates'] += 1
-        preroll = 2 if args.preroll is None else args.preroll
+        # >= 128 steps and >= 2 updates of pre-roll: the training regime
+        # (general-path physics, contacts, TOI) whatever the horizon
+        preroll = max(2, -(-128 // H)) if args.preroll is None else args.preroll
         for _ in range(preroll * H):
             one_step()
         for _ in range(args.warmup):
@@ -348,6 +418,11 @@ def main():
                                if args.mode == 'ppo' else f'{preroll} env steps'),
                    'align_steps': align,
                    'updates_in_timed_region': state['updates'] if args.mode == 'ppo' else 0,
+                   'window': (f'{args.steps} rollout steps = {args.steps / args.horizon:g} PPO iteration(s) of '
+                              f'{args.horizon} steps, each with its GAE + update'
+                              if args.mode == 'ppo' and args.steps % args.horizon == 0 else
+                              (f'{args.steps} rollout steps + {state["updates"]} update(s) of {args.horizon} steps'
+                               if args.mode == 'ppo' else None)),
                    'parallelism': f'env-shard x{world}',
                    'streams_per_gpu': args.shards,
                    'phys_general_envs_last_step': diag['phys_general_envs'],
@@ -375,6 +450,17 @@ def main():
             line['roofline']['traffic'] = tr_['traffic_bytes_per_step'] * n_launch / n
             line['roofline']['traffic_source'] = f'profiles/{tname} (FETCH_SIZE+WRITE_SIZE per mas_step)'
             break
+    if args.flush_stats:
+        env.flush_stats()
+        torch.cuda.synchronize()
+    if rank == 0 and world == 1 and not args.no_live_traffic and os.environ.get('MAS_BENCH_CHILD') != '1':
+        lt = live_traffic(args, n)
+        line['roofline']['traffic_live'] = lt
+        if 'traffic_bytes_per_step' in lt:
+            line['roofline']['traffic'] = lt['traffic_bytes_per_step'] * n_launch / n
+            line['roofline']['traffic_source'] = ('measured in this run: FETCH_SIZE + WRITE_SIZE per mas_step over '
+                                                  'the timed window, two rocprofv3 --pmc child runs of this command '
+                                                  '(raw counters; calibrated value in traffic_live)')
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(args.config, all_cores=args.cpu_all_cores)
     if rank == 0:

@@ -24,6 +24,7 @@ using namespace mas;
 namespace mas {
 struct ClassInfo {
     int words, w_rng, w_has32, w_stats, w_cont, w_invdt, lds_bytes;
+    int am, post_union;  // agent slots; k_post_lanes' LDS union bytes (the in-place reset's permutation scratch)
 };
 #define MAS_DECLARE(NAME)                                                                                     \
     ClassInfo class_info_##NAME();                                                                          \
@@ -857,10 +858,11 @@ int mas_reset(mas_handle* h, const uint8_t* env_mask, float* obs, void* stream)
     return MAS_OK;
 }
 
-int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, uint8_t* done, int32_t auto_reset,
-             void* stream)
+// mas_step / mas_step_x: xrow non-null writes bf16 policy-input rows instead
+// of the fp32 obs rows
+static int step_impl(mas_handle* h, const int8_t* actions, float* obs, uint16_t* xrow, int64_t x_ld, float* rewards,
+                     uint8_t* done, int32_t auto_reset, void* stream)
 {
-    if (!h || !actions || !obs || !rewards || !done) return fail(MAS_ERR_INVALID_ARG, "mas_step: null argument");
     dim3 g((unsigned)((h->N + kWG - 1) / kWG));
     if (h->split && !h->sp_made) {
         int cur = 0;
@@ -886,6 +888,8 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
     // host decision per step: neither may be captured, so while the caller's
     // stream is capturing (hipStreamIsCapturing) the step runs on one stream.
     Params P = h->P;
+    P.xrow = xrow;
+    P.x_ld = x_ld;
     if (h->par) std::swap(P.slow_count, P.slow_prev);
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing((hipStream_t)stream, &cap));
@@ -917,6 +921,42 @@ int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, u
     HIP_TRY(hipGetLastError());
     h->par ^= 1;
     return MAS_OK;
+}
+
+int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards, uint8_t* done, int32_t auto_reset,
+             void* stream)
+{
+    if (!h || !actions || !obs || !rewards || !done) return fail(MAS_ERR_INVALID_ARG, "mas_step: null argument");
+    return step_impl(h, actions, obs, nullptr, 0, rewards, done, auto_reset, stream);
+}
+
+// why mas_step_x cannot run this handle (nullptr: it can)
+static const char* step_x_refusal(const mas_handle* h, int32_t auto_reset)
+{
+    const mas_config& c = h->cfg;
+    if (c.lidar_n_lasers != 0) return "mas_step_x: the lidars key (k_lidar writes fp32 columns): use mas_step";
+    const int am = h->ops.info.am > 0 ? h->ops.info.am : 1;
+    if (auto_reset && c.grid_size * c.grid_size * (64 / am) > h->ops.info.post_union)
+        return "mas_step_x: this config's auto-reset runs in the fp32 reset launch (spawn grid too large for the "
+               "in-place reset): use mas_step";
+    return nullptr;
+}
+
+int mas_step_x_supported(const mas_handle* h, int32_t auto_reset)
+{
+    if (!h) return fail(MAS_ERR_INVALID_ARG, "mas_step_x_supported: null handle");
+    return step_x_refusal(h, auto_reset) ? 0 : 1;
+}
+
+int mas_step_x(mas_handle* h, const int8_t* actions, void* x_bf16, int64_t x_stride, float* rewards, uint8_t* done,
+               int32_t auto_reset, void* stream)
+{
+    if (!h || !actions || !x_bf16 || !rewards || !done) return fail(MAS_ERR_INVALID_ARG, "mas_step_x: null argument");
+    if (x_stride < h->P.D || (x_stride % 4) != 0 || (reinterpret_cast<uintptr_t>(x_bf16) & 7))
+        return fail(MAS_ERR_INVALID_ARG, "mas_step_x: x_stride must be a multiple of 4 >= obs_dim, x 8-B aligned");
+    if (const char* why = step_x_refusal(h, auto_reset)) return fail(MAS_ERR_UNSUPPORTED, why);
+    return step_impl(h, actions, nullptr, reinterpret_cast<uint16_t*>(x_bf16), x_stride, rewards, done, auto_reset,
+                     stream);
 }
 
 int mas_flush_stats(mas_handle* h, float* stats, void* stream)
@@ -1114,6 +1154,21 @@ int mas_policy_act_rows(const void* packed, int32_t obs_dim, int64_t n_rows, int
         return fail(MAS_ERR_INVALID_ARG, "mas_policy_act: misaligned buffer (obs/x 16 B, actions 2 B)");
     HIP_TRY(policy_act(packed, obs_dim, n_rows, obs, x_bf16, x_stride, seed, step, first_row, actions, logp, value,
                        (hipStream_t)stream));
+    return MAS_OK;
+}
+
+int mas_policy_act_x(const void* packed, int32_t obs_dim, int64_t n_rows, int64_t first_row, const void* x_bf16,
+                     int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp, float* value,
+                     void* stream)
+{
+    if (!packed || obs_dim <= 0 || n_rows <= 0 || first_row < 0 || !x_bf16 || !actions || !logp || !value)
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_act_x: bad argument");
+    if (!policy_x_ok(obs_dim, x_stride) || (reinterpret_cast<uintptr_t>(x_bf16) & 15) ||
+        (reinterpret_cast<uintptr_t>(actions) & 1))
+        return fail(MAS_ERR_INVALID_ARG, "mas_policy_act_x: x 16-B aligned with a padded row stride (a multiple "
+                                         "of 8 >= 16*ceil(obs_dim/16)), actions 2-B aligned");
+    HIP_TRY(policy_act(packed, obs_dim, n_rows, nullptr, const_cast<void*>(x_bf16), x_stride, seed, step, first_row,
+                       actions, logp, value, (hipStream_t)stream));
     return MAS_OK;
 }
 

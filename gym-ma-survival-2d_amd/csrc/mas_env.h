@@ -126,6 +126,10 @@ struct Params {
                          // while the list is shorter than the grid (the slow list: the divergent SolveTOI
                          // chains of two slow envs in one wave would run one after the other)
     unsigned long long* prof;  // MAS_PROFILE builds only: per-phase wave time accumulators
+    // mas_step_x: the observation rows go out as bf16 policy-input rows
+    // (xrow[(e * A + i) * x_ld + c], columns c < D; nullptr: f32 obs rows)
+    uint16_t* xrow;
+    int64_t x_ld;
 };
 
 constexpr int kListShards = 64;   // shards of the general-path list (Params::list_shards)

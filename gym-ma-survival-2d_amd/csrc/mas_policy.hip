@@ -410,8 +410,11 @@ constexpr int kHeadN[6] = {3, 3, 3, 2, 2, 2};
 constexpr int kHeadOff[6] = {0, 3, 6, 9, 11, 13};
 
 // KS > 0: compile-time k-step count (obs_dim in (16 (KS-1), 16 KS]) with every
-// x fragment loaded up front; KS == 0: any obs_dim, chunked layer 1
-template <int KS>
+// x fragment loaded up front; KS == 0: any obs_dim, chunked layer 1.
+// XIN: the input rows are bf16 rows xb [M][xb_stride] already (mas_step_x
+// wrote them; columns past obs_dim hold the bias column and zeros, which meet
+// W1's zero padding), read instead of fp32 obs and not written back
+template <int KS, bool XIN>
 __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
                                                              int64_t M, const float* __restrict__ obs,
                                                              __bf16* __restrict__ xb, int64_t xb_stride,
@@ -436,7 +439,28 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
     const int64_t row = row0 + (l & 31);
     const bool ok = row < M;
     bf8 h1[kMT][2], h2[kMT][2];
-    if constexpr (KS > 0) {
+    if constexpr (XIN) {
+        // bf16 rows: 16-B loads of the lane's 8 columns per k-step, an
+        // out-of-range lane's row clamped into range and zeroed
+        const int64_t rr = ok ? row : M - 1;
+        const __bf16* xr = xb + rr * xb_stride + 8 * h;
+        if constexpr (KS > 0) {
+            bf8 x[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const bf8 v = *reinterpret_cast<const bf8*>(xr + 16 * ks);
+                x[ks] = ok ? v : bf8{};
+            }
+            layer1_reg<KS>(S, F + Lo.w1(), B1, l, on, x, h1);
+        } else {
+            layer1(S, F + Lo.w1(), B1, ks1, l, on,
+                   [&](int ks) {
+                       const bf8 v = *reinterpret_cast<const bf8*>(xr + 16 * ks);
+                       return ok ? v : bf8{};
+                   },
+                   h1);
+        }
+    } else if constexpr (KS > 0) {
         bf8 x[KS];
         if ((D & 3) == 0 && D == 16 * KS) {  // every k-step complete: branch-free loads
             const int64_t rr = ok ? row : M - 1;
@@ -1832,7 +1856,12 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
                       hipStream_t s)
 {
     const int ks1 = (D + 15) / 16;
-    auto k = ks1 == 10 ? pol::k_policy_act<10> : ks1 == 9 ? pol::k_policy_act<9> : pol::k_policy_act<0>;
+    // obs == nullptr: the bf16 rows in xb are the input (mas_policy_act_x)
+    const bool xin = obs == nullptr;
+    auto k = xin ? (ks1 == 10 ? pol::k_policy_act<10, true> : ks1 == 9 ? pol::k_policy_act<9, true>
+                                                                       : pol::k_policy_act<0, true>)
+                 : (ks1 == 10 ? pol::k_policy_act<10, false> : ks1 == 9 ? pol::k_policy_act<9, false>
+                                                                        : pol::k_policy_act<0, false>);
     hipLaunchKernelGGL(k, dim3((unsigned)act_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
                        ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, first_row, act, logp, value);
     return hipGetLastError();

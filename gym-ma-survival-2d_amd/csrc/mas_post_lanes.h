@@ -593,6 +593,79 @@ struct QuadRow {
     }
 };
 
+// bf16 rows for mas_step_x (the PPO consumer's policy input): the same
+// columns, each rounded to bf16 (round to nearest even: the conversion the
+// policy kernels apply to fp32 obs rows, so the policy sees the same bits).
+__device__ __forceinline__ uint32_t bf16x2(float a, float b)
+{
+    const __bf16 x = (__bf16)a, y = (__bf16)b;
+    return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+
+// QuadRow into bf16 rows (row stride ld elements, ld % 4 == 0, 8-B aligned
+// base): the same LDS swap, each store writes 4 columns (8 B) of one row,
+// a 32-B run of one row per env and instruction
+struct QuadRowX {
+    uint16_t* env;  // x row 0 of the env
+    float4* stg;
+    int i;
+    int64_t ld;
+    bool on;
+    int k = 0;
+    float b[16];
+    __device__ __forceinline__ void put(float v)
+    {
+        const int s = k & 15;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (s == q) b[q] = v;
+        if (s == 15) flush(k - 15, 16);
+        ++k;
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if ((k & 15) != 0) flush(k - (k & 15), k & 15);
+    }
+    __device__ __forceinline__ void flush(int g0, int n)
+    {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * q < n) stg[i * 4 + q] = make_float4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float4 v = stg[r * 4 + i];
+            if (on && 4 * i < n)
+                *reinterpret_cast<uint2*>(env + (int64_t)r * ld + g0 + 4 * i) = make_uint2(bf16x2(v.x, v.y), bf16x2(v.z, v.w));
+        }
+    }
+};
+
+// SeqRow into one bf16 row: 8-B stores of 4 columns (ld % 4 == 0, 8-B
+// aligned base), the last partial group column by column
+struct SeqRowX {
+    uint16_t* p;
+    int k = 0;
+    float b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, b3 = 0.0f;
+    __device__ __forceinline__ void put(float v)
+    {
+        const int s = k & 3;
+        if (s == 0) b0 = v;
+        else if (s == 1) b1 = v;
+        else if (s == 2) b2 = v;
+        else b3 = v;
+        if (s == 3) *reinterpret_cast<uint2*>(p + (k - 3)) = make_uint2(bf16x2(b0, b1), bf16x2(b2, b3));
+        ++k;
+    }
+    __device__ __forceinline__ void finish()
+    {
+        const int s = k & 3, g = k - s;
+        const float v[3] = {b0, b1, b2};
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (q < s) p[g + q] = (uint16_t)(bf16x2(v[q], 0.0f) & 0xffffu);
+    }
+};
+
 // EX: the config fills the class exactly (A, B, H at the class maxima, no
 // lasers) with Teams = P.teams: every count is a compile-time constant, so
 // the whole row unrolls and each column's index -- the sink's buffer slot and
@@ -947,8 +1020,17 @@ inline bool reset_fits_post(const Params& P)
 #ifndef MAS_POST_OCC
 #define MAS_POST_OCC 3
 #endif
+// test builds: MAS_POST_VGPR=n caps the kernel at n VGPRs for every class
+// (the xl / ffa classes are LDS-bound and otherwise take ~230), to run the
+// parity suites on a heavily spilling schedule
+#ifdef MAS_POST_VGPR
+#define MAS_POST_BOUNDS \
+    __launch_bounds__(kWG, MAS_POST_OCC) __attribute__((amdgpu_waves_per_eu(512 / MAS_POST_VGPR, 512 / MAS_POST_VGPR)))
+#else
+#define MAS_POST_BOUNDS __launch_bounds__(kWG, MAS_POST_OCC)
+#endif
 template <class C, int M>
-__global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint32_t* __restrict__ state, int64_t N,
+__global__ MAS_POST_BOUNDS void k_post_lanes(Params P, uint32_t* __restrict__ state, int64_t N,
                                                        float* __restrict__ obs, float* __restrict__ rew,
                                                        uint8_t* __restrict__ done, int ar)
 {
@@ -1501,7 +1583,20 @@ __global__ __launch_bounds__(kWG, MAS_POST_OCC) void k_post_lanes(Params P, uint
 #if MAS_POST_OBS_SEQ
     const uintptr_t ob = reinterpret_cast<uintptr_t>(obs);
     const bool ex = A == C::AM && P.B == C::BM && P.H == C::HM && P.n_lasers == 0;
-    if (C::AM == 4 && ex && (D & 3) == 0 && (ob & 15) == 0) {
+    if (P.xrow) {
+        // mas_step_x: bf16 policy-input rows (x_ld % 4 == 0, 8-B aligned:
+        // checked on the host), the same row writer
+        if (C::AM == 4 && ex && (D & 3) == 0) {
+            QuadRowX o{P.xrow + e * (int64_t)A * P.x_ld, reinterpret_cast<float4*>(&lds.u) + j * 16, i, P.x_ld, valid};
+            if (P.teams) write_obs_row_seq<C, true, true>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+            else write_obs_row_seq<C, true, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+        } else if (row_on) {
+            SeqRowX o{P.xrow + (e * A + i) * P.x_ld};
+            if (ex && P.teams) write_obs_row_seq<C, true, true>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+            else if (ex) write_obs_row_seq<C, true, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+            else write_obs_row_seq<C, false, false>(V, P, alive_m, i, lastmeta, lhx, lhy, o);
+        }
+    } else if (C::AM == 4 && ex && (D & 3) == 0 && (ob & 15) == 0) {
         // every lane (the swaps need the env's four), stores by `valid`
         static_assert(C::AM != 4 || sizeof(lds.u) >= sizeof(float4) * 16 * S, "the staging fits the union");
         QuadRow o{obs + e * (int64_t)(A * D), reinterpret_cast<float4*>(&lds.u) + j * 16, i, D, valid};

@@ -56,6 +56,8 @@ SIGNATURES = {
     'mas_seed': (c_int32, [c_void_p, POINTER(c_uint64), c_void_p]),
     'mas_reset': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_step': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    'mas_step_x': (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p]),
+    'mas_step_x_supported': (c_int32, [c_void_p, c_int32]),
     'mas_flush_stats': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'mas_state_bytes': (c_int64, [c_void_p]),
     'mas_get_state': (c_int32, [c_void_p, c_void_p, c_void_p]),
@@ -79,6 +81,8 @@ SIGNATURES = {
                                  ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_policy_act_rows': (c_int32, [c_void_p, c_int32, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                       ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'mas_policy_act_x': (c_int32, [c_void_p, c_int32, c_int64, c_int64, c_void_p, c_int64, ctypes.c_uint64,
+                                   ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_policy_train': (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                    c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
                          + [c_void_p] * 7),

@@ -74,6 +74,10 @@ class PPOConfig:
     # process group has more than one rank; True forces them at world size 1
     # too (the one-GPU RCCL test runs the exact calls of the 8-GPU bench)
     allreduce: Optional[bool] = None
+    # fused path: the env writes the policy's bf16 input rows itself
+    # (mas_step_x) instead of fp32 obs rows the act kernel re-reads and
+    # converts; None = whenever the env supports it (same bits either way)
+    x_obs: Optional[bool] = None
 
 
 def _split_k(m: int, cap: int = int(os.environ.get('MAS_SPLITK_CAP', '64'))) -> int:
@@ -330,6 +334,19 @@ class FusedPolicy:
                                            ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(logp.data_ptr()),
                                            ctypes.c_void_p(value.data_ptr()), self._stream()))
 
+    @torch.no_grad()
+    def act_x(self, xb, seed, step, actions, logp, value, first_row=0):
+        """act over bf16 input rows xb [M, Dx] (x_buffer layout, e.g. written by
+        mas_step_x): the same actions, log-probs and values as act on the fp32
+        rows they were rounded from; xb is not written."""
+        M = xb.shape[0]
+        assert xb.is_contiguous() and xb.dtype == torch.bfloat16 and xb.shape[1] == self.Dx
+        assert actions.is_contiguous() and logp.is_contiguous() and value.is_contiguous()
+        check(self.lib.mas_policy_act_x(ctypes.c_void_p(self.packed.data_ptr()), self.D, M, int(first_row),
+                                        ctypes.c_void_p(xb.data_ptr()), self.Dx, int(seed), int(step),
+                                        ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(logp.data_ptr()),
+                                        ctypes.c_void_p(value.data_ptr()), self._stream()))
+
     def _buffers_rm(self, M):
         if self._bufs is None or self._bufs['M'] != M:
             bf = dict(dtype=torch.bfloat16, device=self.device)
@@ -540,7 +557,7 @@ class RolloutBuffer:
         self.ret = torch.zeros((T, N, A), **f)
         self.adv_sums = torch.zeros((2,), device=device, dtype=torch.float64)
         self.gae_scratch = None  # mas_gae's partial sums (made at the first HIP GAE call)
-        self.xb = None  # fused path: bf16 policy-input rows [T, N*A, Dp] written by mas_policy_act
+        self.xb = None  # fused path: bf16 policy-input rows [T (+1 with x_obs), N*A, Dx] (mas_policy_act / mas_step_x)
 
 
 def _allreduce_grads(params, world, group=None):
@@ -594,10 +611,18 @@ class PPOTrainer:
             fused = self.device.type == 'cuda' and cfg.hidden == 256
         self.fused = None
         self.fused_opt = None
+        self.x_obs = False
         if fused:
             self.fused = FusedPolicy(self.policy, env.obs_dim, self.device)
             b = self.buf
-            self.buf.xb = self.fused.x_buffer(b.T, b.N * b.A)
+            xo = cfg.x_obs
+            if xo is None:
+                xo = hasattr(env, 'supports_step_x') and env.supports_step_x()
+            self.x_obs = bool(xo)
+            # x_obs: rows T + 1 (the env writes step t's next rows into t + 1)
+            self.buf.xb = self.fused.x_buffer(b.T + (1 if self.x_obs else 0), b.N * b.A)
+            if self.x_obs:
+                self._set_x0(self.buf.obs[0])
             M = b.N * b.A
             self._boot = (torch.empty((M, 6), dtype=torch.int8, device=self.device),
                           torch.empty((M,), dtype=torch.float32, device=self.device))
@@ -606,6 +631,13 @@ class PPOTrainer:
                 self.fused_opt = FusedAdam(self.policy.parameters(), self.opt, self.fused.lib, self.device)
         else:
             self._sync_rollout_policy()
+
+    @torch.no_grad()
+    def _set_x0(self, obs):
+        """x_obs: the first rollout rows from fp32 obs [N, A, D] (a reset's,
+        or a checkpoint's): rounded to bf16 as the kernels round."""
+        b = self.buf
+        b.xb[0][:, :b.D].copy_(obs.reshape(-1, b.D).to(torch.bfloat16))
 
     def _fwd(self, x):
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.cfg.autocast_bf16):
@@ -634,12 +666,26 @@ class PPOTrainer:
             for e, s, lo, hi in self.env.shard_slices():
                 with torch.cuda.stream(s):
                     r0, r1 = lo * A, hi * A
+                    if self.x_obs:
+                        self.fused.act_x(b.xb[t][r0:r1], self.seed, self.steps_taken,
+                                         b.actions[t].view(-1, 6)[r0:r1], b.logp[t].view(-1)[r0:r1],
+                                         b.values[t].view(-1)[r0:r1], first_row=r0)
+                        e.step_x(b.actions[t][lo:hi], b.xb[t + 1][r0:r1], b.rewards[t][lo:hi], b.dones[t][lo:hi])
+                        continue
                     self.fused.act(b.obs[t].view(-1, D)[r0:r1], self.seed, self.steps_taken,
                                    b.actions[t].view(-1, 6)[r0:r1], b.logp[t].view(-1)[r0:r1],
                                    b.values[t].view(-1)[r0:r1], xb=b.xb[t][r0:r1], first_row=r0)
                     e.step(b.actions[t][lo:hi], out=(b.obs[t + 1][lo:hi], b.rewards[t][lo:hi], b.dones[t][lo:hi]))
             self.env.join()
             self.steps_taken += 1
+            return
+        if self.x_obs:
+            # the env wrote these rows (bf16) at the last step; it writes the
+            # next ones into row block t + 1
+            self.fused.act_x(b.xb[t], self.seed, self.steps_taken, b.actions[t].view(-1, 6), b.logp[t].view(-1),
+                             b.values[t].view(-1))
+            self.steps_taken += 1
+            self.env.step_x(b.actions[t], b.xb[t + 1], b.rewards[t], b.dones[t])
             return
         if self.fused is not None:
             self.fused.act(b.obs[t].view(-1, b.D), self.seed, self.steps_taken, b.actions[t].view(-1, 6),
@@ -664,7 +710,9 @@ class PPOTrainer:
     @torch.no_grad()
     def finish_rollout(self):
         b, c = self.buf, self.cfg
-        if self.fused is not None:
+        if self.x_obs:
+            self.fused.act_x(b.xb[c.horizon], self.seed, 0, self._boot[0], self._boot[1], b.values[c.horizon].view(-1))
+        elif self.fused is not None:
             self.fused.act(b.obs[c.horizon].view(-1, b.D), self.seed, 0, self._boot[0], self._boot[1],
                            b.values[c.horizon].view(-1))
         else:
@@ -708,7 +756,10 @@ class PPOTrainer:
                 self.fused.pack()
         self.last_stats = {'loss': loss.detach(), 'pg': pg.detach(), 'v': vl.detach(), 'entropy': ent.detach(),
                            'clipfrac': cf.detach()}
-        b.obs[0].copy_(b.obs[c.horizon])
+        if self.x_obs:
+            b.xb[0].copy_(b.xb[c.horizon])
+        else:
+            b.obs[0].copy_(b.obs[c.horizon])
 
     def update(self):
         if self.fused is not None:
@@ -753,6 +804,8 @@ class PPOTrainer:
         sd = {'policy': self.policy.state_dict(), 'opt': self.opt.state_dict(),
               'steps_taken': int(self.steps_taken), 'seed': int(self.seed),
               'gen': self.gen.get_state(), 'obs0': self.buf.obs[0].detach().clone()}
+        if self.x_obs:
+            sd['xb0'] = self.buf.xb[0].detach().clone()  # (x_obs: the next rollout's rows; obs0 is the reset's)
         if hasattr(self.env, 'get_state'):
             sd['env'] = self.env.get_state().detach().clone()
             if hasattr(self.env, 'state_meta'):
@@ -784,6 +837,11 @@ class PPOTrainer:
                     raise ValueError(f'checkpoint env state does not match this env: {diff}')
             self.env.set_state(sd['env'].to(self.device))
         self.buf.obs[0].copy_(sd['obs0'])
+        if self.x_obs:
+            if 'xb0' in sd:
+                self.buf.xb[0].copy_(sd['xb0'])
+            else:
+                self._set_x0(self.buf.obs[0])
         if self.fused is not None:
             self.fused.pack()
         else:

@@ -148,6 +148,27 @@ class VecMaSurvival:
                                  int(self.auto_reset), self._stream()))
         return obs, rew, done, {}
 
+    def supports_step_x(self) -> bool:
+        """mas_step_x can run this env (no lidars; an auto-reset in place)."""
+        return bool(self._lib.mas_step_x_supported(self._h, int(self.auto_reset)))
+
+    def step_x(self, actions, x, rewards, dones):
+        """mas_step writing the observation rows as bf16 policy-input rows:
+        x bf16 [N * A, Dx] (or [N, A, Dx]), Dx a multiple of 4 >= obs_dim;
+        columns [0, obs_dim) are written (the fp32 rows of `step` rounded to
+        bf16), the rest untouched.  rewards [N, A] fp32, dones [N] uint8.
+        actions as for `step` (int8, contiguous, on this device)."""
+        torch = _torch()
+        N, A = self.n_envs, self.n_agents
+        if tuple(actions.shape) != (N, A, 6) or actions.dtype != torch.int8 or not actions.is_contiguous():
+            raise ValueError('actions must be contiguous int8 [N, A, 6]')
+        if x.dtype != torch.bfloat16 or not x.is_contiguous() or x.numel() % (N * A) != 0:
+            raise ValueError('x must be contiguous bf16 [N * A, Dx]')
+        Dx = x.numel() // (N * A)
+        check(self._lib.mas_step_x(self._h, ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(x.data_ptr()), Dx,
+                                   ctypes.c_void_p(rewards.data_ptr()), ctypes.c_void_p(dones.data_ptr()),
+                                   int(self.auto_reset), self._stream()))
+
     def flush_stats(self):
         """Per-env stats accumulated since the last flush, float [N, 19]
         (reward0..7, kills0..7, steps, heals_used, boxes_placed)."""
@@ -360,6 +381,9 @@ class ShardedVecMaSurvival:
         """Sum over the shards of VecMaSurvival.invalid_actions (synchronises)."""
         self.join()
         return sum(e.invalid_actions(reset) for e in self.envs)
+
+    def supports_step_x(self) -> bool:
+        return all(e.supports_step_x() for e in self.envs)
 
     def flush_stats(self):
         self.join()

@@ -132,6 +132,21 @@ int mas_reset(mas_handle* h, const uint8_t* env_mask, float* obs, void* stream);
 int mas_step(mas_handle* h, const int8_t* actions, float* obs, float* rewards,
              uint8_t* done, int32_t auto_reset, void* stream);
 
+/* mas_step with the observation rows written as the PPO consumer's bf16
+ * policy input instead of fp32 obs: x_bf16 [n_envs * n_agents][x_stride]
+ * (x_stride a multiple of 4 >= obs_dim, 8-B aligned), columns [0, obs_dim)
+ * of each row = the fp32 row of mas_step rounded to bf16 (round to nearest
+ * even, the conversion mas_policy_act applies to fp32 rows), the other
+ * columns untouched (the caller's bias column and padding stay).  Rewards,
+ * done and the env state are those of mas_step, bit for bit.  Not for the
+ * lidars key or a config whose auto-reset runs in the separate reset launch
+ * (MAS_ERR_UNSUPPORTED: use mas_step).  No reference equivalent (the rollout
+ * side). */
+int mas_step_x(mas_handle* h, const int8_t* actions, void* x_bf16, int64_t x_stride, float* rewards,
+               uint8_t* done, int32_t auto_reset, void* stream);
+/* 1 when mas_step_x can run this handle with this auto_reset, else 0. */
+int mas_step_x_supported(const mas_handle* h, int32_t auto_reset);
+
 /* Per-env episode statistics (flush_stats, masurvival_env.py:471-508):
  * device float [n_envs][MAS_STATS_WIDTH] laid out as
  * [0,8) reward0..reward{R-1}, [8,16) kills0..kills{R-1}, 16 steps,
@@ -238,6 +253,13 @@ int mas_policy_act(const void* packed, int32_t obs_dim, int64_t n_rows, const fl
 int mas_policy_act_rows(const void* packed, int32_t obs_dim, int64_t n_rows, int64_t first_row, const float* obs,
                         void* x_bf16, int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp,
                         float* value, void* stream);
+/* mas_policy_act_x: mas_policy_act_rows over bf16 input rows x_bf16
+ * [n_rows][x_stride] (mas_step_x's rows: columns past obs_dim are ignored --
+ * W1 is zero there), which are not written; the same actions, log-probs and
+ * values as mas_policy_act_rows on the fp32 rows they were rounded from. */
+int mas_policy_act_x(const void* packed, int32_t obs_dim, int64_t n_rows, int64_t first_row, const void* x_bf16,
+                     int64_t x_stride, uint64_t seed, uint64_t step, int8_t* actions, float* logp, float* value,
+                     void* stream);
 int mas_policy_train(const void* packed, int32_t obs_dim, int64_t n_rows, const void* x_bf16, int64_t x_stride,
                      const int8_t* actions, const float* old_logp, const float* adv, const float* ret, float clip,
                      float vf_coef, float ent_coef, float scale, void* h1, void* h2, void* da1, void* da2, void* dz,

@@ -41,6 +41,16 @@ def per_step(path, counter, last):
     return {k: v / n for k, v in tot.items()}, len(steps)
 
 
+def kernel_bytes(path, counter, name):
+    """The counter's bytes (KB -> B) summed over every dispatch of kernel `name`
+    (e.g. k_stats, the calibration kernel of bench.py's live_traffic)."""
+    tot = 0.0
+    for r in csv.DictReader(open(path)):
+        if r['Counter_Name'] == counter and (name + '(') in r['Kernel_Name']:
+            tot += float(r['Counter_Value']) * 1024.0
+    return tot
+
+
 def main(fetch_csv, write_csv, out, workload, last=None):
     f, nf = per_step(fetch_csv, 'FETCH_SIZE', last)
     w, nw = per_step(write_csv, 'WRITE_SIZE', last)

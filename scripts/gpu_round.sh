@@ -50,56 +50,63 @@ for step in "$@"; do
       cd $R && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $? ;;
     bench)
       cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_driver.log 2>&1 || exit $?
-      cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $? ;;
+      cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline --no-live-traffic > $O/bench.log 2>&1 || exit $? ;;
     benchcw0)
       # the PPO update on k_policy_train (MAS_POL_CW=0): the counted-wait kernel's A/B
-      cd $R && MAS_POL_CW=0 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_cw0.log 2>&1 || exit $? ;;
+      cd $R && MAS_POL_CW=0 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/bench_driver_cw0.log 2>&1 || exit $? ;;
     benchq)
-      cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $?
-      cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver.log 2>&1 || exit $? ;;
+      cd $R && timeout -k 10 400 python bench.py --no-cpu-baseline --no-live-traffic > $O/bench.log 2>&1 || exit $?
+      cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/bench_driver.log 2>&1 || exit $? ;;
     shards)
-      cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --shards 2 --no-cpu-baseline > $O/bench_driver_shards2.log 2>&1 || exit $?
-      cd $R && timeout -k 10 400 python bench.py --shards 2 --no-cpu-baseline > $O/bench_shards2.log 2>&1 || exit $? ;;
+      cd $R && timeout -k 10 400 python bench.py --steps 20 --warmup 5 --shards 2 --no-cpu-baseline --no-live-traffic > $O/bench_driver_shards2.log 2>&1 || exit $?
+      cd $R && timeout -k 10 400 python bench.py --shards 2 --no-cpu-baseline --no-live-traffic > $O/bench_shards2.log 2>&1 || exit $? ;;
+    shardab)
+      # env handles per GPU on concurrent streams (bench.py --shards): 1, 2, 4, alternating, twice; driver window
+      for k in 1 2; do
+        for sh in 1 2 4; do
+          cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --shards $sh --no-cpu-baseline --no-live-traffic >> $O/shardab_driver_sh$sh.json 2>> $O/shardab.err || exit 1
+        done
+      done ;;
     env)
-      cd $R && timeout -k 10 200 python bench.py --mode env --no-cpu-baseline > $O/bench_env.log 2>&1 || exit $?
-      cd $R && timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_ffa.log 2>&1 || exit $?
-      cd $R && timeout -k 10 200 python bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline > $O/bench_1v1.log 2>&1 || exit $? ;;
+      cd $R && timeout -k 10 200 python bench.py --mode env --no-cpu-baseline --no-live-traffic > $O/bench_env.log 2>&1 || exit $?
+      cd $R && timeout -k 10 200 python bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline --no-live-traffic > $O/bench_ffa.log 2>&1 || exit $?
+      cd $R && timeout -k 10 200 python bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline --no-live-traffic > $O/bench_1v1.log 2>&1 || exit $? ;;
     full)
       # the C4 / C5 workloads at their configured env counts on one GPU
-      cd $R && timeout -k 10 300 python bench.py --mode env --envs 262144 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_env_c4full.log 2>&1 || exit $?
-      cd $R && timeout -k 10 300 python bench.py --mode env --config ffa4 --envs 131072 --steps 30 --warmup 10 --no-cpu-baseline > $O/bench_env_c5full.log 2>&1 || exit $? ;;
+      cd $R && timeout -k 10 300 python bench.py --mode env --envs 262144 --steps 50 --warmup 10 --no-cpu-baseline --no-live-traffic > $O/bench_env_c4full.log 2>&1 || exit $?
+      cd $R && timeout -k 10 300 python bench.py --mode env --config ffa4 --envs 131072 --steps 30 --warmup 10 --no-cpu-baseline --no-live-traffic > $O/bench_env_c5full.log 2>&1 || exit $? ;;
     c4rank)
       # the C4 per-rank workload of the 8-GPU target (2v2 x 262144 over 8 GPUs = 32768 per rank) in the
       # driver-shaped PPO window: bench line, kernel trace, FETCH / WRITE passes
-      cd $R && timeout -k 10 300 python bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_c4rank.log 2>&1 || exit $?
-      cd $R && timeout -k 10 300 python bench.py --envs 32768 --no-cpu-baseline > $O/bench_c4rank.log 2>&1 || exit $?
+      cd $R && timeout -k 10 300 python bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/bench_driver_c4rank.log 2>&1 || exit $?
+      cd $R && timeout -k 10 300 python bench.py --envs 32768 --no-cpu-baseline --no-live-traffic > $O/bench_c4rank.log 2>&1 || exit $?
       cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4rank -o run -- \
-        python3 $R/bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_c4rank.log 2>&1 || exit $?
+        python3 $R/bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/prof_c4rank.log 2>&1 || exit $?
       for c in FETCH_SIZE WRITE_SIZE; do
         cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "mas::k_" --output-format csv \
-          -d $O/pmc_${c}_c4rank -o run -- python3 $R/bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_${c}_c4rank.log 2>&1 || exit $?
+          -d $O/pmc_${c}_c4rank -o run -- python3 $R/bench.py --envs 32768 --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/pmc_${c}_c4rank.log 2>&1 || exit $?
       done ;;
     envprof2)
       cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_env -o run -- \
-        python3 $R/bench.py --mode env --no-cpu-baseline > $O/prof_env.log 2>&1 || exit $? ;;
+        python3 $R/bench.py --mode env --no-cpu-baseline --no-live-traffic > $O/prof_env.log 2>&1 || exit $? ;;
     prof)
       cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- \
-        python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.log 2>&1 || exit $?
+        python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/prof_bench.log 2>&1 || exit $?
       cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench128 -o run -- \
-        python3 $R/bench.py --no-cpu-baseline > $O/prof_bench128.log 2>&1 || exit $? ;;
+        python3 $R/bench.py --no-cpu-baseline --no-live-traffic > $O/prof_bench128.log 2>&1 || exit $? ;;
     profd)
       cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- \
-        python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.log 2>&1 || exit $? ;;
+        python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/prof_bench.log 2>&1 || exit $? ;;
     pmc)
       cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "mas::k_" --output-format csv \
-        -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || exit $?
+        -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/pmc_fetch.log 2>&1 || exit $?
       cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mas::k_" --output-format csv \
-        -d $O/pmc_write -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_write.log 2>&1 || exit $? ;;
+        -d $O/pmc_write -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/pmc_write.log 2>&1 || exit $? ;;
     envprof)
       cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_ffa -o run -- \
-        python3 $R/bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline > $O/prof_ffa.log 2>&1 || exit $?
+        python3 $R/bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline --no-live-traffic > $O/prof_ffa.log 2>&1 || exit $?
       cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_1v1 -o run -- \
-        python3 $R/bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline > $O/prof_1v1.log 2>&1 || exit $? ;;
+        python3 $R/bench.py --mode env --config 1v1 --steps 100 --warmup 20 --no-cpu-baseline --no-live-traffic > $O/prof_1v1.log 2>&1 || exit $? ;;
     profenv)
       # phase timers of the env kernels (libmas_prof.so, `make -C gym-ma-survival-2d_amd/csrc prof`)
       cd $R && timeout -k 10 300 python -u profiles/prof_env.py 2v2 65536 20 --ppo > $O/prof_env_ppo.txt 2>&1 || exit $?
@@ -111,15 +118,15 @@ for step in "$@"; do
     split0ab)
       # the slow split (default) vs one stream (MAS_SPLIT=0), alternating processes: driver window, env-only 2v2
       for sp in 2 0 2 0; do
-        cd $R && MAS_SPLIT=$sp timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/split0ab_driver_sp$sp.json 2>> $O/split0ab.err || exit 1
-        cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline >> $O/split0ab_env_sp$sp.json 2>> $O/split0ab.err || exit 1
+        cd $R && MAS_SPLIT=$sp timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic >> $O/split0ab_driver_sp$sp.json 2>> $O/split0ab.err || exit 1
+        cd $R && MAS_SPLIT=$sp timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline --no-live-traffic >> $O/split0ab_env_sp$sp.json 2>> $O/split0ab.err || exit 1
       done ;;
     slowkab*)
       # MAS_SLOW_K (TOI events of an env's step that send it to the slow list next step), alternating:
       # slowkab = 4 (default) vs 2 vs 1; slowkab:<k>,<k>,... those values
       KS="4 2 1"; [ "$step" != slowkab ] && KS=$(echo ${step#slowkab:} | tr ',' ' ')
       for k in $KS $KS; do
-        cd $R && MAS_SLOW_K=$k timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline >> $O/slowkab_driver_k$k.json 2>> $O/slowkab.err || exit 1
+        cd $R && MAS_SLOW_K=$k timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic >> $O/slowkab_driver_k$k.json 2>> $O/slowkab.err || exit 1
       done ;;
     libab:*)
       # libab:<variant>: driver window + env-only 2v2, default library vs masurvival/_lib/libmas_<variant>.so, alternating
@@ -127,8 +134,8 @@ for step in "$@"; do
       for k in 1 2; do
         for lib in default $V; do
           L=""; [ $lib != default ] && L="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$lib.so"
-          cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $L >> $O/libab_driver_$lib.json 2>> $O/libab.err || exit 1
-          cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline $L >> $O/libab_env_$lib.json 2>> $O/libab.err || exit 1
+          cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic $L >> $O/libab_driver_$lib.json 2>> $O/libab.err || exit 1
+          cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline --no-live-traffic $L >> $O/libab_env_$lib.json 2>> $O/libab.err || exit 1
         done
       done ;;
     varab:*)
@@ -138,9 +145,9 @@ for step in "$@"; do
       LIB=""; [ "$V" != main ] && LIB="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$V.so"
       for k in 1 2; do
         for val in $(echo $VALS | tr ',' ' '); do
-          cd $R && env $VAR=$val timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $LIB >> $O/varab_${V}_driver_$VAR$val.json 2>> $O/varab.err || exit 1
-          cd $R && env $VAR=$val timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline $LIB >> $O/varab_${V}_env_$VAR$val.json 2>> $O/varab.err || exit 1
-          cd $R && env $VAR=$val timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline $LIB >> $O/varab_${V}_ffa_$VAR$val.json 2>> $O/varab.err || exit 1
+          cd $R && env $VAR=$val timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic $LIB >> $O/varab_${V}_driver_$VAR$val.json 2>> $O/varab.err || exit 1
+          cd $R && env $VAR=$val timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline --no-live-traffic $LIB >> $O/varab_${V}_env_$VAR$val.json 2>> $O/varab.err || exit 1
+          cd $R && env $VAR=$val timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline --no-live-traffic $LIB >> $O/varab_${V}_ffa_$VAR$val.json 2>> $O/varab.err || exit 1
         done
       done ;;
     libabx:*)
@@ -148,9 +155,9 @@ for step in "$@"; do
       for k in 1 2; do
         for v in $(echo ${step#libabx:} | tr ',' ' '); do
           LIB=""; [ "$v" != main ] && LIB="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
-          cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $LIB >> $O/libabx_driver_$v.json 2>> $O/libabx.err || exit 1
-          cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline $LIB >> $O/libabx_env_$v.json 2>> $O/libabx.err || exit 1
-          cd $R && timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline $LIB >> $O/libabx_ffa_$v.json 2>> $O/libabx.err || exit 1
+          cd $R && timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic $LIB >> $O/libabx_driver_$v.json 2>> $O/libabx.err || exit 1
+          cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline --no-live-traffic $LIB >> $O/libabx_env_$v.json 2>> $O/libabx.err || exit 1
+          cd $R && timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline --no-live-traffic $LIB >> $O/libabx_ffa_$v.json 2>> $O/libabx.err || exit 1
         done
       done ;;
     pmcenv)
@@ -159,26 +166,26 @@ for step in "$@"; do
         set -- $cfg
         for c in FETCH_SIZE WRITE_SIZE; do
           cd /tmp && timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "mas::k_" --output-format csv \
-            -d $O/pmc_${c}_$1_$2 -o run -- python3 $R/bench.py --mode env --config $1 --envs $2 --steps $3 --warmup $4 --no-cpu-baseline > $O/pmc_${c}_$1_$2.log 2>&1 || exit 1
+            -d $O/pmc_${c}_$1_$2 -o run -- python3 $R/bench.py --mode env --config $1 --envs $2 --steps $3 --warmup $4 --no-cpu-baseline --no-live-traffic > $O/pmc_${c}_$1_$2.log 2>&1 || exit 1
         done
       done ;;
     sqmix)
       # SQ instruction mix of the env kernels in the driver-shaped bench (one counter set, its own run)
       cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-        --kernel-include-regex "mas::k_" --output-format csv -d $O/pmc_sq -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/pmc_sq.log 2>&1 || exit 1 ;;
+        --kernel-include-regex "mas::k_" --output-format csv -d $O/pmc_sq -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic > $O/pmc_sq.log 2>&1 || exit 1 ;;
     ktrace:*)
       # ktrace:<lib>[,<lib>...]: kernel traces of the PPO bench per library (main = libmas.so)
       for v in $(echo ${step#ktrace:} | tr ',' ' '); do
         LIB=""; [ "$v" != main ] && LIB="--lib $R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
         cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$v -o run -- \
-          python3 $R/bench.py --no-cpu-baseline $LIB > $O/kt_$v.log 2>&1 || exit 1
+          python3 $R/bench.py --no-cpu-baseline --no-live-traffic $LIB > $O/kt_$v.log 2>&1 || exit 1
       done ;;
     ktraced:*)
       # ktraced:<lib>[,<lib>...]: kernel traces of the driver-window bench (20 steps, 1 update) per library
       for v in $(echo ${step#ktraced:} | tr ',' ' '); do
         LIB=""; [ "$v" != main ] && LIB="--lib $R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
         cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktd_$v -o run -- \
-          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline $LIB > $O/ktd_$v.log 2>&1 || exit 1
+          python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-live-traffic $LIB > $O/ktd_$v.log 2>&1 || exit 1
       done ;;
     ktraceenv:*)
       # ktraceenv:<config>:<steps>:<lib>[,<lib>...]: kernel traces of the env-only bench per library
@@ -186,7 +193,7 @@ for step in "$@"; do
       for v in $(echo $LIBS | tr ',' ' '); do
         LIB=""; [ "$v" != main ] && LIB="--lib $R/gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
         cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_${CFG}_$v -o run -- \
-          python3 $R/bench.py --mode env --config $CFG --steps $ST --warmup 10 --no-cpu-baseline $LIB > $O/kt_${CFG}_$v.log 2>&1 || exit 1
+          python3 $R/bench.py --mode env --config $CFG --steps $ST --warmup 10 --no-cpu-baseline --no-live-traffic $LIB > $O/kt_${CFG}_$v.log 2>&1 || exit 1
       done ;;
     dist)
       # multi-rank rehearsal on one GPU: 2 ranks over gloo (test + bench launch path)

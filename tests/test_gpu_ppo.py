@@ -106,15 +106,18 @@ def test_hip_sampler_logp_and_distribution():
     assert torch.equal(acts, acts3)
 
 
-def test_sharded_rollout_matches_one_handle():
+@pytest.mark.parametrize('x_obs', [False, True])
+def test_sharded_rollout_matches_one_handle(x_obs):
     """ShardedVecMaSurvival (3 handles on 3 streams, per-shard act with the
-    global row key) fills the rollout buffer bit-identically to one handle."""
+    global row key) fills the rollout buffer bit-identically to one handle
+    (x_obs: each shard writes its bf16 policy rows, mas_step_x)."""
     from masurvival.vec_env import ShardedVecMaSurvival
     n, T = 4096, 6
     tr = []
     for env in (VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n)),
                 ShardedVecMaSurvival(C3_CONFIG, n_envs=n, shards=3, seeds=range(n))):
-        t_ = PPOTrainer(env, PPOConfig(horizon=8), seed=0)
+        t_ = PPOTrainer(env, PPOConfig(horizon=8, x_obs=x_obs), seed=0)
+        assert t_.x_obs == x_obs
         for t in range(T):
             t_.rollout_step(t)
         tr.append(t_)
@@ -124,7 +127,7 @@ def test_sharded_rollout_matches_one_handle():
         assert torch.equal(getattr(b1, name)[:T + 1], getattr(b2, name)[:T + 1]), name
     for name in ('actions', 'logp', 'rewards', 'dones'):
         assert torch.equal(getattr(b1, name)[:T], getattr(b2, name)[:T]), name
-    assert torch.equal(b1.xb[:T], b2.xb[:T])
+    assert torch.equal(b1.xb[:T + (1 if x_obs else 0)], b2.xb[:T + (1 if x_obs else 0)])
     for t_ in tr:
         t_.env.close()
 
@@ -136,8 +139,8 @@ def _vec(n, seeds, shards):
     return ShardedVecMaSurvival(C3_CONFIG, n_envs=n, shards=shards, seeds=seeds, auto_reset=True)
 
 
-@pytest.mark.parametrize('shards', [1, 2])
-def test_checkpoint_resume_on_env(tmp_path, shards):
+@pytest.mark.parametrize('shards,x_obs', [(1, False), (2, False), (1, True), (2, True)])
+def test_checkpoint_resume_on_env(tmp_path, shards, x_obs):
     """PPOTrainer.save after an iteration, load into a fresh trainer on a fresh
     env: the next rollout (fused act kernel + env kernels) is bit-identical to
     the run that never stopped -- policy, env state and sampling counters all
@@ -146,12 +149,12 @@ def test_checkpoint_resume_on_env(tmp_path, shards):
     n, T = 1024, 8
     trs = []
     env = _vec(n, list(range(n)), shards)
-    tr = PPOTrainer(env, PPOConfig(horizon=T), seed=0)
+    tr = PPOTrainer(env, PPOConfig(horizon=T, x_obs=x_obs), seed=0)
     tr.iteration()
     path = str(tmp_path / 'ckpt.pt')
     tr.save(path)
     env2 = _vec(n, list(range(1000, 1000 + n)), shards)
-    tr2 = PPOTrainer(env2, PPOConfig(horizon=T), seed=5)
+    tr2 = PPOTrainer(env2, PPOConfig(horizon=T, x_obs=x_obs), seed=5)
     tr2.load(path)
     for t_ in (tr, tr2):
         for t in range(T):
@@ -162,10 +165,40 @@ def test_checkpoint_resume_on_env(tmp_path, shards):
     # values[T] is the previous rollout's bootstrap value (finish_rollout),
     # which only the uninterrupted trainer has computed
     assert torch.equal(b1.obs, b2.obs) and torch.equal(b1.values[:T], b2.values[:T])
+    assert torch.equal(b1.xb, b2.xb)
     for name in ('actions', 'logp', 'rewards', 'dones'):
         assert torch.equal(getattr(b1, name), getattr(b2, name)), name
     env.close()
     env2.close()
+
+
+def test_x_obs_trainer_matches_fp32_obs_trainer():
+    """PPOConfig.x_obs: the env writes the policy's bf16 input rows
+    (mas_step_x) and the act kernel reads them (mas_policy_act_x), instead of
+    fp32 obs rows that mas_policy_act rounds to bf16 itself.  Two trainers from
+    the same seeds, two PPO iterations each with auto-reset: every rollout
+    array, the update's input rows and the trained parameters are
+    bit-identical."""
+    n, T = 2048, 8
+    trs = []
+    for xo in (False, True):
+        env = VecMaSurvival(C3_CONFIG, n_envs=n, seeds=range(n), auto_reset=True)
+        tr = PPOTrainer(env, PPOConfig(horizon=T, x_obs=xo), seed=0)
+        assert tr.x_obs == xo
+        for _ in range(2):
+            tr.iteration()
+        trs.append(tr)
+    torch.cuda.synchronize()
+    b1, b2 = trs[0].buf, trs[1].buf
+    for name in ('actions', 'logp', 'values', 'rewards', 'dones', 'adv', 'ret'):
+        assert torch.equal(getattr(b1, name), getattr(b2, name)), name
+    assert torch.equal(b1.xb[:T], b2.xb[:T])  # the update's input rows
+    # the fp32 path's last rows, rounded, are the x path's next rollout's first rows
+    assert torch.equal(b2.xb[0].view(n, -1, b2.xb.shape[-1])[..., :b2.D], b1.obs[0].bfloat16())
+    for p1, p2 in zip(trs[0].policy.parameters(), trs[1].policy.parameters()):
+        assert torch.equal(p1, p2)
+    for tr in trs:
+        tr.env.close()
 
 
 def test_checkpoint_env_mismatch_is_refused(tmp_path):
