@@ -43,11 +43,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 ENVS_DEFAULT = {'1v1': 4096, '2v2': 65536, 'ffa4': 16384}
 
 
-def algorithmic_bytes_per_env_step(A, H, B, D):
+def algorithmic_bytes_per_env_step(A, H, B, D, obs_bytes=4):
     """Bstep = 8*S + 6A + 4*A*D + 4A + 1 with
-    S = 27A + 14B + 3H + 17 + 2*(A(A-1)/2 + A(B+4)) + 4 persistent words."""
+    S = 27A + 14B + 3H + 17 + 2*(A(A-1)/2 + A(B+4)) + 4 persistent words;
+    obs_bytes = 2 when the step writes bf16 policy rows (mas_step_x: 2*A*D)."""
     S = 27 * A + 14 * B + 3 * H + 17 + 2 * (A * (A - 1) // 2 + A * (B + 4)) + 4
-    return 8 * S + 6 * A + 4 * A * D + 4 * A + 1
+    return 8 * S + 6 * A + obs_bytes * A * D + 4 * A + 1
 
 
 def cpu_info():
@@ -304,11 +305,23 @@ def main():
             return r
         return f
 
+    def timed_x(step_fn):  # mas_step_x (the PPO trainer's bf16-row path)
+        def f(*a):
+            e0, e1 = ev(), ev()
+            e0.record()
+            r = step_fn(*a)
+            e1.record()
+            kev.append((e0, e1))
+            return r
+        return f
+
     if args.shards > 1:
         for sub in env.envs:
             sub.step = timed(sub.step)
+            sub.step_x = timed_x(sub.step_x)
     else:
         env.step = timed(env.step)
+        env.step_x = timed_x(env.step_x)
 
     rev, uev = [], []  # whole rollout step / whole GAE + update, on the current stream
     # the horizon: the timed window holds whole PPO iterations when it can
@@ -394,7 +407,8 @@ def main():
 
     diag = env.debug_counters()
     total_agent_steps = world * n * A * args.steps
-    b_env = algorithmic_bytes_per_env_step(A, env.rc.n_heals, env.rc.n_boxes, D)
+    x_obs = args.mode == 'ppo' and tr.x_obs
+    b_env = algorithmic_bytes_per_env_step(A, env.rc.n_heals, env.rc.n_boxes, D, obs_bytes=2 if x_obs else 4)
     n_launch = n // args.shards  # envs per mas_step launch group (per shard when sharded)
     achieved = b_env * n_launch / (kern_ms * 1e-3) / 1e9
     if args.mode == 'ppo':
@@ -436,12 +450,13 @@ def main():
                      'kernel': 'mas_step launch group (k_pre_lanes, k_gen_solve_g, k_post_lanes with the auto-reset in place; the slow-list pair on the side stream)' if args.shards == 1 else
                      f'mas_step launch group of one shard ({args.shards} shards on concurrent streams)',
                      'kernel_ms': kern_ms, 'bytes_per_env_step': b_env,
+                     'obs_rows': ('bf16 policy-input rows (mas_step_x)' if x_obs else 'fp32 obs rows (mas_step)'),
                      'bytes_per_launch': b_env * n_launch},
         'cpu_baseline': None,
     }
     # HBM traffic per mas_step from the committed rocprofv3 PMC passes of this
     # same workload and regime (profiles/pmc_traffic.py); null when none matches
-    key = f'{args.config}:{n}:{args.mode}:preroll{preroll}'
+    key = f'{args.config}:{n}:{args.mode}:preroll{preroll}' + (':x_obs' if x_obs else '')
     for tname in sorted(os.listdir(os.path.join(ROOT, 'profiles')), reverse=True):
         if not (tname.startswith('r0') and 'pmc_traffic' in tname and tname.endswith('.json')):
             continue
@@ -457,10 +472,17 @@ def main():
         lt = live_traffic(args, n)
         line['roofline']['traffic_live'] = lt
         if 'traffic_bytes_per_step' in lt:
-            line['roofline']['traffic'] = lt['traffic_bytes_per_step'] * n_launch / n
+            # the guide's gfx950 correction (FETCH_SIZE counts half the bytes
+            # read), confirmed for this access width by the k_stats
+            # calibration of the same runs when it is present
+            if 'traffic_bytes_per_step_calibrated' in lt:
+                tb, how = lt['traffic_bytes_per_step_calibrated'], 'calibrated on k_stats (traffic_live.calibration)'
+            else:
+                tb, how = 2 * lt['fetch_bytes_per_step'] + lt['write_bytes_per_step'], 'FETCH_SIZE x 2 (guide)'
+            line['roofline']['traffic'] = tb * n_launch / n
             line['roofline']['traffic_source'] = ('measured in this run: FETCH_SIZE + WRITE_SIZE per mas_step over '
-                                                  'the timed window, two rocprofv3 --pmc child runs of this command '
-                                                  '(raw counters; calibrated value in traffic_live)')
+                                                  'the timed window, two rocprofv3 --pmc child runs of this command, '
+                                                  + how + '; raw counters in traffic_live')
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(args.config, all_cores=args.cpu_all_cores)
     if rank == 0:

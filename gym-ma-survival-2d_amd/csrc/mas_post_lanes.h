@@ -1406,10 +1406,15 @@ __global__ MAS_POST_BOUNDS void k_post_lanes(Params P, uint32_t* __restrict__ st
             done[e] = is_done ? 1 : 0;
             float* st = reinterpret_cast<float*>(state);
             // every word's load issued before any add (the per-word
-            // read-modify-write under q < R waited out one load latency each)
+            // read-modify-write under q < R waited out one load latency each);
+            // only the 2R + 1 words this step adds to are loaded
             float cur[17];
 #pragma unroll
-            for (int q = 0; q < 17; ++q) cur[q] = st[state_index(LY::stat + q, e, N)];
+            for (int q = 0; q < 8; ++q) {
+                cur[q] = q < R ? st[state_index(LY::stat + q, e, N)] : 0.0f;
+                cur[8 + q] = q < R ? st[state_index(LY::stat + 8 + q, e, N)] : 0.0f;
+            }
+            cur[16] = st[state_index(LY::stat + 16, e, N)];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 if (q >= R) continue;
@@ -1466,7 +1471,12 @@ __global__ MAS_POST_BOUNDS void k_post_lanes(Params P, uint32_t* __restrict__ st
         if (sb) slot_store<S, LY::kBoxW>(lds.box, state, N, lds.eidx, LY::box, sb);
         if (si) slot_store<S, LY::kItemW>(lds.item, state, N, lds.eidx, LY::item, si);
         if (sh) slot_store<S, LY::kHealW>(lds.heal, state, N, lds.eidx, LY::heal, sh);
-        if (sv) slot_store<S, LY::kZoneW>(lds.zone, state, N, lds.eidx, LY::zone, sv);
+        // the zone's mutable words only (phase, timers, endgame, the current
+        // zone): the phase centres change only at a reset, whose path below
+        // stores the whole group (saves 16 of 23 words per env and step)
+        constexpr int kZM = PV::kZPhase;
+        static_assert(LY::kZoneW - kZM == 7, "the zone's mutable words follow the centres");
+        if (sv) slot_store<S, LY::kZoneW - kZM>(lds.zone + kZM * S, state, N, lds.eidx, LY::zone + kZM, sv);
     }
     // ---------------- auto-reset: the done envs ----------------
     if (ar && P.reset_in_post) {

@@ -617,7 +617,9 @@ class PPOTrainer:
             b = self.buf
             xo = cfg.x_obs
             if xo is None:
-                xo = hasattr(env, 'supports_step_x') and env.supports_step_x()
+                # MAS_X_OBS=0 in the environment: the fp32 obs path (A/B runs)
+                xo = (os.environ.get('MAS_X_OBS', '1') != '0' and hasattr(env, 'supports_step_x')
+                      and env.supports_step_x())
             self.x_obs = bool(xo)
             # x_obs: rows T + 1 (the env writes step t's next rows into t + 1)
             self.buf.xb = self.fused.x_buffer(b.T + (1 if self.x_obs else 0), b.N * b.A)

@@ -41,6 +41,10 @@ for step in "$@"; do
             >> $O/gae_bench.txt 2>&1 || exit 1
         done
       fi ;;
+    py:*)
+      # py:<script>[,arg...]: one python script (repo-relative), output to <tag>/py_<name>.txt
+      IFS=, read -r SCR ARGS <<< "${step#py:}"
+      cd $R && timeout -k 10 300 python -u $SCR $(echo $ARGS | tr ',' ' ') > $O/py_$(basename $SCR .py).txt 2>&1 || exit 1 ;;
     ab)
       cd $R && timeout -k 10 600 python -u scripts/ab_solve_golden.py all > $O/ab_golden.log 2>&1 || { echo "A/B differs"; exit 1; } ;;
     regimes)
