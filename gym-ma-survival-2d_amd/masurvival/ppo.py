@@ -80,7 +80,7 @@ class PPOConfig:
     x_obs: Optional[bool] = None
 
 
-def _split_k(m: int, cap: int = int(os.environ.get('MAS_SPLITK_CAP', '64'))) -> int:
+def _split_k(m: int, cap: int = int(os.environ.get('MAS_SPLITK_CAP', '128'))) -> int:
     c = 1
     while c < cap and m % (2 * c) == 0 and m // (2 * c) >= 4096:
         c *= 2
