@@ -30,9 +30,9 @@ SHORT_ZONE = {'phases': 5, 'cooldown': 12, 'damage': 6, 'radiuses': [10, 5, 2.5,
 @pytest.mark.parametrize('name,cfg,n,T', [
     ('C1 1v1 (SeqRowX)', C1_CONFIG, 512, 200),
     ('C3 2v2 (QuadRowX)', C3_CONFIG, 1024, 200),
-    ('C5 ffa4 (QuadRowX)', C5_CONFIG, 256, 120),
+    ('C5 ffa4 (QuadRowX)', dict(C5_CONFIG, safe_zone=SHORT_ZONE), 256, 120),
     ('3 agents in the 2v2 class (SeqRowX)', dict(THREE, safe_zone=SHORT_ZONE), 512, 160),
-    ('6 agents, xl (SeqRowX)', SIX, 128, 120)])
+    ('6 agents, xl (SeqRowX)', dict(SIX, safe_zone=SHORT_ZONE), 128, 120)])
 def test_step_x_rows_are_the_rounded_fp32_rows(name, cfg, n, T):
     try:
         ref = VecMaSurvival(cfg, n_envs=n, seeds=range(n), auto_reset=True)
