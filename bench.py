@@ -338,20 +338,42 @@ def main():
         H = pcfg.horizon
         state = {'t': 0, 'updates': 0}
 
+        # Every event record is a marker packet on the stream (~4-5 us of GPU
+        # time between two kernels, r06m trace; events without the
+        # system-scope fence measured the same), so the window records two per
+        # rollout step: before k_pre and after the last env kernel (the env
+        # step's pair, kev).  The rollout step runs from the previous boundary
+        # event (the last env step's end, or the update's end) to this step's
+        # env end, and the GAE + update from that env end to one event after
+        # the update.
+        shared = args.shards == 1
+        state['edge'] = None
+
         def one_step():
-            e0, e1 = ev(), ev()
-            e0.record()
-            tr.rollout_step(state['t'])
-            e1.record()
+            if shared:
+                if state['edge'] is None:
+                    state['edge'] = ev()
+                    state['edge'].record()
+                e0 = state['edge']
+                tr.rollout_step(state['t'])
+                e1 = kev[-1][1]  # the env step's end event (timed_x), the rollout step's last work
+                state['edge'] = e1
+            else:
+                e0, e1 = ev(), ev()
+                e0.record()
+                tr.rollout_step(state['t'])
+                e1.record()
             rev.append((e0, e1))
             state['t'] += 1
             if state['t'] == H:
-                u0, u1 = ev(), ev()
-                u0.record()
+                u0, u1 = (state['edge'], ev()) if shared else (ev(), ev())
+                if not shared:
+                    u0.record()
                 tr.finish_rollout()
                 tr.update()
                 u1.record()
                 uev.append((u0, u1))
+                state['edge'] = u1
                 state['t'] = 0
                 state['updates'] += 1
         # >= 128 steps and >= 2 updates of pre-roll: the training regime
@@ -385,6 +407,7 @@ def main():
     uev.clear()
     if args.mode == 'ppo':
         state['updates'] = 0
+        state['edge'] = None  # the window's first rollout step starts at a fresh event
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -875,8 +875,11 @@ static int step_impl(mas_handle* h, const int8_t* actions, float* obs, uint16_t*
         const char* pv = getenv("MAS_SIDE_PRIO");
         const bool prio = !(pv && pv[0] == '0');
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->sp.side, hipStreamNonBlocking, prio ? hi : lo);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.fork, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.join, hipEventDisableTiming);
+        // fork / join order work between two streams of this device only: a
+        // device-scope release (no system-scope cache writeback + invalidate
+        // at each record, which a default event carries)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.fork, hipEventDisableTiming | hipEventReleaseToDevice);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->sp.join, hipEventDisableTiming | hipEventReleaseToDevice);
         (void)hipSetDevice(cur);
         HIP_TRY(e);
         h->sp_made = true;

@@ -404,22 +404,45 @@ class FusedPolicy:
                           'part': torch.empty((nb, 4), dtype=torch.float32, device=self.device)}
         return self._bufs
 
-    def _dw(self, a, h, F, M):
-        """(a[:, :M] @ h[:256, :M]^T, a.sum(1)) in fp32 via mas_policy_dw."""
+    def _dw(self, a, h, F, M, into=None):
+        """(a[:, :M] @ h[:256, :M]^T, a.sum(1)) in fp32 via mas_policy_dw.
+        into: (weight, bias) fp32 tensors that are one contiguous span of
+        F * 256 + F floats (the flat gradient buffer of FusedAdam): the sums
+        land there directly and (None, None) is returned."""
         key = ('dw', F, M)
         if key not in self._dwbuf:
             n = int(self.lib.mas_policy_dw_scratch(F, 256, M))
             self._dwbuf[key] = (torch.empty((n,), dtype=torch.float32, device=self.device),
                                 torch.empty((F * 256 + F,), dtype=torch.float32, device=self.device))
         scratch, out = self._dwbuf[key]
+        optr = into[0].data_ptr() if into is not None else out.data_ptr()
         check(self.lib.mas_policy_dw(F, 256, M, ctypes.c_void_p(a.data_ptr()), a.stride(0), ctypes.c_void_p(h.data_ptr()),
-                                     h.stride(0), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                                     h.stride(0), ctypes.c_void_p(optr), ctypes.c_void_p(scratch.data_ptr()),
                                      self._stream()))
+        if into is not None:
+            return None, None
         return out[:F * 256].view(F, 256), out[F * 256:]
 
-    def grads(self, xb, actions, old_logp, adv, ret, cfg: 'PPOConfig'):
+    @staticmethod
+    def _grad_span(w, b):
+        """(w.grad, b.grad) when they are one contiguous fp32 span, weight then
+        bias (FusedAdam's flat buffer), else None."""
+        gw, gb = w.grad, b.grad
+        if gw is None or gb is None or gw.dtype != torch.float32 or gb.dtype != torch.float32:
+            return None
+        if not (gw.is_contiguous() and gb.is_contiguous()):
+            return None
+        if gw.untyped_storage().data_ptr() != gb.untyped_storage().data_ptr():
+            return None
+        if gb.data_ptr() != gw.data_ptr() + 4 * gw.numel():
+            return None
+        return gw, gb
+
+    def grads(self, xb, actions, old_logp, adv, ret, cfg: 'PPOConfig', stats: bool = True):
         """Sets .grad of the policy parameters to the gradient of the PPO loss
-        (mean over the M rows) and returns (loss, pg, v, entropy, clipfrac)."""
+        (mean over the M rows) and returns (loss, pg, v, entropy, clipfrac);
+        stats=False skips those reductions (the update keeps only the last
+        minibatch's) and returns None."""
         M = xb.shape[0]
         assert xb.dtype == torch.bfloat16 and xb.shape[1] == self.Dx and xb.is_contiguous()
         for t in (actions, old_logp, adv, ret):
@@ -437,14 +460,15 @@ class FusedPolicy:
         l1, l2, l3 = p.body[0], p.body[2], p.head
         # layers 2 / 3: the split-K MFMA kernel (mas_policy_dw) where enabled,
         # else the split-K GEMM over the ones-row trick; layer 1 reads x
-        # row-major: a GEMM
+        # row-major: a GEMM.  With FusedAdam's flat gradient buffer the dW
+        # kernels' sums land in .grad directly (no copy launches)
         if '3' in _DW_LAYERS and M % 32 == 0:
-            g3w, g3b = self._dw(B['dz'], B['h2'], 16, M)
+            g3w, g3b = self._dw(B['dz'], B['h2'], 16, M, into=self._grad_span(l3.weight, l3.bias))
         else:
             g3 = _splitk_nt(B['dz'], B['h2'])          # [16, 257]
             g3w, g3b = g3[:, :256], g3[:, 256]
         if '2' in _DW_LAYERS and M % 32 == 0:
-            g2w, g2b = self._dw(B['da2'], B['h1'], 256, M)
+            g2w, g2b = self._dw(B['da2'], B['h1'], 256, M, into=self._grad_span(l2.weight, l2.bias))
         else:
             g2 = _splitk_nt(B['da2'], B['h1'])         # [256, 257]
             g2w, g2b = g2[:, :256], g2[:, 256]
@@ -452,10 +476,14 @@ class FusedPolicy:
         grads = {l3.weight: g3w, l3.bias: g3b, l2.weight: g2w, l2.bias: g2b,
                  l1.weight: g1[:, :self.D], l1.bias: g1[:, self.D]}
         for prm, g in grads.items():
+            if g is None:
+                continue  # written in place above
             if prm.grad is None:
                 prm.grad = g.to(prm.dtype).clone(memory_format=torch.contiguous_format)
             else:
                 prm.grad.copy_(g)
+        if not stats:
+            return None
         s = B['part'].sum(0) / M
         pg, v, ent, clipfrac = s[0], s[1], s[2], s[3]
         return pg + cfg.vf_coef * v - cfg.ent_coef * ent, pg, v, ent, clipfrac
@@ -557,6 +585,7 @@ class RolloutBuffer:
         self.ret = torch.zeros((T, N, A), **f)
         self.adv_sums = torch.zeros((2,), device=device, dtype=torch.float64)
         self.gae_scratch = None  # mas_gae's partial sums (made at the first HIP GAE call)
+        self.adv_stats = None    # [sum, sum of squares, count] of the advantages (finish_rollout)
         self.xb = None  # fused path: bf16 policy-input rows [T (+1 with x_obs), N*A, Dx] (mas_policy_act / mas_step_x)
 
 
@@ -724,8 +753,13 @@ class PPOTrainer:
             b.gae_scratch = gae_scratch(b.N * b.A, self.device)
         self.gae_impl(b.rewards, b.values, b.dones, c.gamma, c.lam, b.adv, b.ret, b.adv_sums, self.env.n_agents,
                       scratch=b.gae_scratch)
-        stats = torch.cat([b.adv_sums, torch.tensor([float(b.adv.numel())], device=self.device,
-                                                     dtype=torch.float64)])
+        if b.adv_stats is None:
+            # [sum, sum of squares, count]: the count is set once (no host copy per iteration)
+            b.adv_stats = torch.full((3,), float(b.adv.numel()), device=self.device, dtype=torch.float64)
+        stats = b.adv_stats
+        stats[:2].copy_(b.adv_sums)
+        if self.collectives:
+            stats[2].fill_(float(b.adv.numel()))  # the all-reduce below sums the counts in place
         if self.collectives:
             dist.all_reduce(stats, group=self.group)
         mean = stats[0] / stats[2]
@@ -737,14 +771,18 @@ class PPOTrainer:
         assert c.horizon % c.minibatches == 0, 'fused update: horizon must split into whole time chunks'
         tc = c.horizon // c.minibatches
         params = list(self.policy.parameters())
-        for _ in range(c.epochs):
+        for ep in range(c.epochs):
             order = torch.randperm(c.minibatches, generator=torch.Generator().manual_seed(self.steps_taken))
-            for k in order.tolist():
+            for n, k in enumerate(order.tolist()):
                 sl = slice(k * tc, (k + 1) * tc)
                 xb = b.xb[sl].reshape(-1, self.fused.Dx)
                 M = xb.shape[0]
-                loss, pg, vl, ent, cf = self.fused.grads(xb, b.actions[sl].reshape(M, 6), b.logp[sl].reshape(M),
-                                                         b.adv[sl].reshape(M), b.ret[sl].reshape(M), c)
+                # last_stats keeps the last minibatch's loss terms: only it reduces them
+                last = ep == c.epochs - 1 and n == c.minibatches - 1
+                st = self.fused.grads(xb, b.actions[sl].reshape(M, 6), b.logp[sl].reshape(M),
+                                      b.adv[sl].reshape(M), b.ret[sl].reshape(M), c, stats=last)
+                if last:
+                    loss, pg, vl, ent, cf = st
                 if self.fused_opt is not None:
                     # flat gradient buffer: one all-reduce, the 1 / world folded into the step
                     if self.collectives:

@@ -1,5 +1,6 @@
-"""Time the fused policy kernels alone (HIP events): mas_policy_act on the
-2v2 rollout batch (65536 envs x 4 agents) and mas_policy_train on one PPO
+"""Time the fused policy kernels alone (HIP events): mas_policy_act (fp32
+rows) and mas_policy_act_x (bf16 rows) on the 2v2 rollout batch (65536 envs
+x 4 agents) and mas_policy_train on one PPO
 minibatch (16 steps x 262144 rows).  usage: policy_bench.py [lib.so ...]"""
 import ctypes
 import os
@@ -37,6 +38,15 @@ def run(lib_path):
     e1.record()
     torch.cuda.synchronize()
     t_act = e0.elapsed_time(e1) / 50
+    # act_x: the rollout's path (bf16 rows mas_step_x wrote, nothing written back)
+    for _ in range(5):
+        fp.act_x(xb, 1, 0, a, lp, v)
+    e0.record()
+    for i in range(50):
+        fp.act_x(xb, 1, i, a, lp, v)
+    e1.record()
+    torch.cuda.synchronize()
+    t_actx = e0.elapsed_time(e1) / 50
     Mt = 16 * M
     xbt = fp.x_buffer(Mt)
     xbt[:, :D] = torch.randn((Mt, D), device='cuda').to(torch.bfloat16)
@@ -67,7 +77,8 @@ def run(lib_path):
     e1.record()
     torch.cuda.synchronize()
     t_grads = e0.elapsed_time(e1) / 5
-    print(f'{os.path.basename(lib_path)}: act {t_act * 1e3:.1f} us (262144 rows), train kernel {t_train:.3f} ms, '
+    print(f'{os.path.basename(lib_path)}: act {t_act * 1e3:.1f} us, act_x {t_actx * 1e3:.1f} us (262144 rows), '
+          f'train kernel {t_train:.3f} ms, '
           f'grads total {t_grads:.3f} ms ({Mt} rows)', flush=True)
 
 
