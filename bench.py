@@ -214,7 +214,8 @@ def parse_args():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-all-cores', action='store_true',
                     help='add the CPU-baseline leg on every CPU this process may use (cpu_baseline leg iv)')
-    ap.add_argument('--lib', default=None, help='alternative libmas*.so (A/B variants)')
+    ap.add_argument('--lib', default=None, type=os.path.abspath,
+                    help='alternative libmas*.so (A/B variants; made absolute: the PMC child runs start elsewhere)')
     ap.add_argument('--no-live-traffic', action='store_true',
                     help='skip the two rocprofv3 PMC child runs that measure roofline.traffic (live_traffic)')
     ap.add_argument('--flush-stats', action='store_true',

@@ -220,6 +220,25 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// XCD-aware block order of the agent-lane kernels (speed only, never
+// correctness).  A one-wave block owns kWG / AM consecutive envs, so with
+// AM >= 4 one 128-B line of a state word row ([word][env], 4-B words) spans
+// two or more blocks; the dispatcher deals blocks round-robin over the 8
+// XCDs (blocks b and b + 8 share one, MI355X_MICROARCH.md), so neighbouring
+// blocks sit on different L2s and each fetches the whole line.  The
+// bijective remap gives every group of XCD-mates one contiguous run of
+// blocks (cdna_hip_programming.md T1).  MAS_XCD_SWZ=0: the plain order.
+#ifndef MAS_XCD_SWZ
+#define MAS_XCD_SWZ 1
+#endif
+__device__ __forceinline__ int64_t xcd_block()
+{
+    const int64_t b = blockIdx.x;
+    if (!MAS_XCD_SWZ) return b;
+    const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 // ---------------------------------------------------------------------------
 // select helpers for runtime indices into register arrays
 // ---------------------------------------------------------------------------

@@ -427,7 +427,7 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
     MAS_PROF(P, -1);
     const int lane = (int)threadIdx.x;
     const int j = lane / AM, i = lane - j * AM;
-    const int64_t e0 = (int64_t)blockIdx.x * S, e = e0 + j;
+    const int64_t e0 = xcd_block() * S, e = e0 + j;  // (XCD-aware block order)
     const bool valid = e < N;
     const int64_t ev = valid ? e : N - 1;
     const int A = P.A;

@@ -1047,7 +1047,8 @@ __global__ MAS_POST_BOUNDS void k_post_lanes(Params P, uint32_t* __restrict__ st
     const int A = P.A;
     // the env of slot j (lanes past the last env, or of an env the other
     // stream owns, stay for the wave's collectives and store nothing)
-    const int64_t k0 = (int64_t)blockIdx.x * S;
+    // (a list's entries in launch order; the envs in the XCD-aware block order)
+    const int64_t k0 = (M == kGenEnvs ? (int64_t)blockIdx.x : xcd_block()) * S;
     bool valid;
     int64_t e;
     if (M == kGenEnvs) {

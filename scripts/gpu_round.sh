@@ -3,7 +3,7 @@
 #   scripts/gpu_round.sh <tag> <step>...   (steps: the case labels below, e.g.
 #   tests t:<files> testslib:<variant> gaebench ab regimes smoke bench benchq benchcw0 shards env full
 #   c4rank envprof2 prof profd envprof pmc pmcenv sqmix profenv profwaves split0ab slowkab
-#   libab:<variant> ktrace:<libs> ktraced:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
+#   libab:<variant> trafab:<libs> ktrace:<libs> ktraced:<libs> ktraceenv:<cfg>:<steps>:<libs> dist
 #   polab[:<libs>] polpmc trend[:<iterations>])
 # writes gpurun_out/<tag>/...; every GPU step has its own time limit and the
 # script stops at the first failing step.
@@ -163,6 +163,12 @@ for step in "$@"; do
           cd $R && timeout -k 10 200 python -u bench.py --mode env --no-cpu-baseline --no-live-traffic $LIB >> $O/libabx_env_$v.json 2>> $O/libabx.err || exit 1
           cd $R && timeout -k 10 200 python -u bench.py --mode env --config ffa4 --steps 50 --warmup 10 --no-cpu-baseline --no-live-traffic $LIB >> $O/libabx_ffa_$v.json 2>> $O/libabx.err || exit 1
         done
+      done ;;
+    trafab:*)
+      # trafab:<lib>[,<lib>...]: the driver window with its live FETCH / WRITE passes (roofline.traffic) per library
+      for v in $(echo ${step#trafab:} | tr ',' ' '); do
+        LIB=""; [ "$v" != main ] && LIB="--lib gym-ma-survival-2d_amd/masurvival/_lib/libmas_$v.so"
+        cd $R && timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $LIB > $O/trafab_driver_$v.json 2>> $O/trafab.err || exit 1
       done ;;
     pmcenv)
       # FETCH_SIZE / WRITE_SIZE passes of the env-only workloads (2v2, FFA4 shard, 1v1, C4 / C5 full)
