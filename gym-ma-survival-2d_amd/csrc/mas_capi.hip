@@ -1019,6 +1019,42 @@ int mas_set_state(mas_handle* h, const void* src, void* stream)
     return MAS_OK;
 }
 
+namespace {
+// the advantages normalised in place (mas_adv_normalize): the statistics in
+// double, the scale in float, with the roundings of the torch expression
+// adv.sub_(mean.float()).div_(var.sqrt().float() + 1e-8) it replaces
+__global__ __launch_bounds__(256) void k_adv_norm(int64_t n, float* __restrict__ adv, const double* __restrict__ st)
+{
+    const double mean = st[0] / st[2];
+    const double v = st[1] / st[2] - mean * mean;
+    const float m = (float)mean;
+    const float sd = (float)sqrt(v > 0.0 ? v : 0.0) + 1e-8f;
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 + 3 < n) {
+        float4 a = *reinterpret_cast<const float4*>(adv + i0);
+        a.x = (a.x - m) / sd;
+        a.y = (a.y - m) / sd;
+        a.z = (a.z - m) / sd;
+        a.w = (a.w - m) / sd;
+        *reinterpret_cast<float4*>(adv + i0) = a;
+    } else {
+        for (int64_t i = i0; i < n; ++i) adv[i] = (adv[i] - m) / sd;
+    }
+}
+}  // namespace
+
+int mas_adv_normalize(int64_t n, float* adv, const double* stats, void* stream)
+{
+    if (n <= 0 || !adv || !stats) return fail(MAS_ERR_INVALID_ARG, "mas_adv_normalize: need n > 0 and non-null pointers");
+    if (reinterpret_cast<uintptr_t>(adv) & 15)
+        return fail(MAS_ERR_INVALID_ARG, "mas_adv_normalize: adv must be 16-B aligned");
+    const int64_t blocks = (n + 1023) / 1024;
+    if (blocks > 0x7fffffff) return fail(MAS_ERR_INVALID_ARG, "mas_adv_normalize: n too large");
+    hipLaunchKernelGGL(k_adv_norm, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n, adv, stats);
+    HIP_TRY(hipGetLastError());
+    return MAS_OK;
+}
+
 int64_t mas_gae_scratch_doubles(int64_t n_columns)
 {
     return n_columns > 0 ? 2 * ((n_columns + kGaeCols - 1) / kGaeCols) : -1;

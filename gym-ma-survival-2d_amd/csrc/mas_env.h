@@ -92,7 +92,8 @@ struct Params {
     int* phys_count;  // number of them: appended by k_pre, zeroed by the first post kernel on the caller's
                       // stream once the general path (its only reader) is done (graph-replay safe)
     // The general-path list in list_shards shards (kListShards, or 1): k_pre
-    // block b appends to shard b % list_shards -- its entries at
+    // block b appends to shard xcd_block() / ceil(blocks / list_shards)
+    // (b % list_shards with MAS_XCD_SWZ=0) -- its entries at
     // phys_list[shard * list_cap ..], its count at phys_count[shard *
     // kShardStride] -- so that no single counter takes every wave's atomic
     // (memory-side atomics on one address serialise: round 4's one counter
@@ -237,6 +238,24 @@ __device__ __forceinline__ int64_t xcd_block()
     if (!MAS_XCD_SWZ) return b;
     const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+// the general-path list in XCD-aware order too: contiguous k_pre shards,
+// the general kernel in runs of 16 waves (MAS_LIST_XCD=0: round 6's r06p order)
+#ifndef MAS_LIST_XCD
+#define MAS_LIST_XCD 1
+#endif
+// the same in runs of K consecutive blocks per XCD, dealt round-robin (a
+// grid whose first blocks alone have work -- the general kernel over its
+// list -- keeps every XCD busy); the last nb % 8K blocks keep their order
+template <int K>
+__device__ __forceinline__ int64_t xcd_block_run()
+{
+    const int64_t b = blockIdx.x;
+    if (!MAS_XCD_SWZ || !MAS_LIST_XCD) return b;
+    const int64_t nb = gridDim.x, full = nb - nb % (8 * K);
+    if (b >= full) return b;
+    const int64_t x = b % 8, i = b / 8;
+    return (i / K) * (8 * K) + x * K + i % K;
 }
 
 // ---------------------------------------------------------------------------

@@ -786,8 +786,14 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
         const bool mine = lead && !ok && slow == (q == 1);
         const uint64_t m = __ballot(mine);
         if (m == 0ull) continue;
-        // the general-path list: this block's shard (Params::list_shards)
-        const int sh = q ? 0 : (int)(blockIdx.x % (unsigned)P.list_shards);
+        // the general-path list: this block's shard (Params::list_shards):
+        // with the XCD-aware order, shard s takes the s-th run of
+        // ceil(blocks / shards) blocks (a contiguous env range: the general
+        // kernel's XCD-mates then read the lines the range shares), else
+        // every list_shards-th block; at most ceil(blocks / shards) blocks
+        // either way (list_cap)
+        const unsigned bps = (gridDim.x + (unsigned)P.list_shards - 1) / (unsigned)P.list_shards;
+        const int sh = q ? 0 : (MAS_XCD_SWZ && MAS_LIST_XCD ? (int)(xcd_block() / bps) : (int)(blockIdx.x % (unsigned)P.list_shards));
         int* list = q ? P.slow_list : P.phys_list + (int64_t)sh * P.list_cap;
         int* count = q ? P.slow_count : P.phys_count + sh * kShardStride;
         const int64_t cap = q ? N : (int64_t)P.list_cap;

@@ -65,6 +65,7 @@ SIGNATURES = {
     'mas_gae': (c_int32, [c_int32, c_int64, c_int32, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'mas_gae_scratch_doubles': (c_int64, [c_int64]),
+    'mas_adv_normalize': (c_int32, [c_int64, c_void_p, c_void_p, c_void_p]),
     'mas_debug_counters': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_debug_guards': (c_int32, [c_void_p, POINTER(c_int64)]),
     'mas_debug_force_general': (c_int32, [c_void_p, c_int32]),

@@ -204,6 +204,18 @@ def gae(rewards, values, dones, gamma, lam, adv_out, ret_out, sums_out, n_agents
                       ctypes.c_void_p(s)))
 
 
+def adv_normalize(adv, stats, stream=None):
+    """adv (DEVICE fp32, contiguous) normalised in place from stats = fp64
+    [sum, sum of squares, count] (include/masurvival.h mas_adv_normalize):
+    adv.sub_(mean.float()).div_(var.sqrt().float() + 1e-8), one launch."""
+    assert adv.is_cuda and adv.dtype == torch.float32 and adv.is_contiguous()
+    assert stats.dtype == torch.float64 and stats.numel() == 3 and stats.is_contiguous()
+    lib = load_library()
+    st = stream if stream is not None else torch.cuda.current_stream(adv.device).cuda_stream
+    check(lib.mas_adv_normalize(adv.numel(), ctypes.c_void_p(adv.data_ptr()), ctypes.c_void_p(stats.data_ptr()),
+                                ctypes.c_void_p(st)))
+
+
 def gae_reference(rewards, values, dones, gamma, lam, n_agents):
     """Plain torch fp32 restatement of mas_gae (the numerics test's reference)."""
     T = rewards.shape[0]
@@ -583,9 +595,13 @@ class RolloutBuffer:
         self.dones = torch.zeros((T, N), device=device, dtype=torch.uint8)
         self.adv = torch.zeros((T, N, A), **f)
         self.ret = torch.zeros((T, N, A), **f)
-        self.adv_sums = torch.zeros((2,), device=device, dtype=torch.float64)
+        # [sum, sum of squares, count] of the advantages: mas_gae writes the
+        # sums into the first two (adv_sums is that view), the count is set
+        # here (no host copy per iteration)
+        self.adv_stats = torch.zeros((3,), device=device, dtype=torch.float64)
+        self.adv_stats[2] = float(T * N * A)
+        self.adv_sums = self.adv_stats[:2]
         self.gae_scratch = None  # mas_gae's partial sums (made at the first HIP GAE call)
-        self.adv_stats = None    # [sum, sum of squares, count] of the advantages (finish_rollout)
         self.xb = None  # fused path: bf16 policy-input rows [T (+1 with x_obs), N*A, Dx] (mas_policy_act / mas_step_x)
 
 
@@ -753,18 +769,17 @@ class PPOTrainer:
             b.gae_scratch = gae_scratch(b.N * b.A, self.device)
         self.gae_impl(b.rewards, b.values, b.dones, c.gamma, c.lam, b.adv, b.ret, b.adv_sums, self.env.n_agents,
                       scratch=b.gae_scratch)
-        if b.adv_stats is None:
-            # [sum, sum of squares, count]: the count is set once (no host copy per iteration)
-            b.adv_stats = torch.full((3,), float(b.adv.numel()), device=self.device, dtype=torch.float64)
-        stats = b.adv_stats
-        stats[:2].copy_(b.adv_sums)
+        stats = b.adv_stats  # (b.adv_sums is its first two entries)
         if self.collectives:
             stats[2].fill_(float(b.adv.numel()))  # the all-reduce below sums the counts in place
-        if self.collectives:
             dist.all_reduce(stats, group=self.group)
-        mean = stats[0] / stats[2]
-        var = (stats[1] / stats[2] - mean * mean).clamp_min(0.0)
-        b.adv.sub_(mean.float()).div_(var.sqrt().float() + 1e-8)
+        if self.gae_impl is gae and b.adv.is_cuda:
+            # one launch (include/masurvival.h mas_adv_normalize), the roundings of the expression below
+            adv_normalize(b.adv, stats)
+        else:
+            mean = stats[0] / stats[2]
+            var = (stats[1] / stats[2] - mean * mean).clamp_min(0.0)
+            b.adv.sub_(mean.float()).div_(var.sqrt().float() + 1e-8)
 
     def _update_fused(self):
         b, c = self.buf, self.cfg

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define MAS_ABI_VERSION 2  /* 2: mas_gae takes the caller's partial-sum scratch */
+#define MAS_ABI_VERSION 3  /* 2: mas_gae takes the caller's partial-sum scratch; 3: mas_adv_normalize */
 
 #define MAS_OK 0
 #define MAS_ERR_INVALID_ARG (-1)
@@ -184,6 +184,14 @@ int64_t mas_gae_scratch_doubles(int64_t n_columns);
 int mas_gae(int32_t T, int64_t n_columns, int32_t n_agents, const float* rewards, const float* values,
             const uint8_t* done, float gamma, float lam, float* advantages, float* returns, double* adv_sums,
             double* scratch, void* stream);
+/* mas_adv_normalize: the n advantages (DEVICE float, 16-B aligned)
+ * normalised in place from stats = DEVICE double[3] (sum, sum of squares,
+ * count: mas_gae's adv_sums and the count, summed over ranks):
+ *   mean = sum / count, var = max(sum_sq / count - mean^2, 0)   (double)
+ *   adv  = (adv - (float)mean) / ((float)sqrt(var) + 1e-8f)     (float)
+ * one launch, the roundings of the torch expression it replaces
+ * (adv.sub_(mean.float()).div_(var.sqrt().float() + 1e-8)). */
+int mas_adv_normalize(int64_t n, float* adv, const double* stats, void* stream);
 
 /* Rollout side: sample the six action heads (MultiDiscrete [3,3,3,2,2,2]) of
  * n_rows agent rows from logits [n_rows][row_stride] (first 15 floats of a

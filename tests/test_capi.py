@@ -30,7 +30,7 @@ def test_library_exports_all_symbols():
     for s in header_symbols():
         assert hasattr(lib, s), s
     lib.mas_abi_version.restype = ctypes.c_int32
-    assert lib.mas_abi_version() == 2
+    assert lib.mas_abi_version() == 3
 
 
 def test_create_rejects_bad_config_without_gpu():

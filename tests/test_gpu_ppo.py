@@ -9,7 +9,7 @@ torch = pytest.importorskip('torch')
 pytestmark = pytest.mark.gpu
 
 from masurvival.config import C3_CONFIG  # noqa: E402
-from masurvival.ppo import PPOConfig, PPOTrainer, gae, gae_reference  # noqa: E402
+from masurvival.ppo import PPOConfig, PPOTrainer, adv_normalize, gae, gae_reference  # noqa: E402
 from masurvival.vec_env import VecMaSurvival  # noqa: E402
 
 
@@ -33,6 +33,33 @@ def test_gae_kernel_matches_reference(T, N, A, scan, monkeypatch):
     torch.testing.assert_close(ret, rr, atol=1e-5, rtol=1e-5)
     assert np.isclose(float(sums[0]), float(adv.double().sum()), rtol=1e-9, atol=1e-6)
     assert np.isclose(float(sums[1]), float((adv.double() ** 2).sum()), rtol=1e-9)
+
+
+@pytest.mark.parametrize('n,shift', [(65536 * 4 * 20, 0.0), (1001, 3.0), (3, -2.0), (4096, 1e4)])
+def test_adv_normalize_matches_torch_bit_exactly(n, shift):
+    """mas_adv_normalize against the torch expression it replaces, on the
+    same fp64 statistics: identical bits (n not a multiple of 4 covers the
+    tail lanes; shift 1e4 makes sum_sq / n - mean^2 cancel)."""
+    g = torch.Generator(device='cuda').manual_seed(n)
+    adv = torch.randn((n,), device='cuda', generator=g) * 3.0 + shift
+    stats = torch.stack([adv.double().sum(), (adv.double() ** 2).sum(),
+                         torch.tensor(float(n), device='cuda', dtype=torch.float64)])
+    mean = stats[0] / stats[2]
+    var = (stats[1] / stats[2] - mean * mean).clamp_min(0.0)
+    ref = adv.clone().sub_(mean.float()).div_(var.sqrt().float() + 1e-8)
+    out = adv.clone()
+    adv_normalize(out, stats)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+
+
+def test_adv_normalize_zero_variance_clamps():
+    """Negative rounding of the variance clamps to 0: (adv - mean) / 1e-8."""
+    adv = torch.full((8,), 2.0, device='cuda')
+    stats = torch.tensor([16.0, 32.0 - 1e-9, 8.0], device='cuda', dtype=torch.float64)
+    adv_normalize(adv, stats)
+    torch.cuda.synchronize()
+    assert torch.equal(adv, torch.zeros_like(adv))
 
 
 @pytest.mark.parametrize('scan', ['0', '1'])
