@@ -136,7 +136,16 @@ def live_traffic(args, n, timeout_s=240):
     prof = shutil.which('rocprofv3')
     if not prof:
         return {'error': 'rocprofv3 not found'}
-    child = [a for a in sys.argv[1:] if a not in ('--cpu-all-cores',)]
+    child, skip = [], False
+    for a in sys.argv[1:]:  # (--lib passed on absolute: the children run in a scratch directory)
+        if skip:
+            skip = False
+        elif a == '--lib':
+            skip = True
+        elif a != '--cpu-all-cores' and not a.startswith('--lib='):
+            child.append(a)
+    if args.lib:
+        child += ['--lib', args.lib]
     child += ['--no-cpu-baseline', '--no-live-traffic', '--flush-stats']
     if not any(a.startswith('--horizon') for a in child):
         child += ['--horizon', str(args.horizon)]
