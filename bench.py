@@ -487,17 +487,8 @@ def main():
                      'bytes_per_launch': b_env * n_launch},
         'cpu_baseline': None,
     }
-    # HBM traffic per mas_step from the committed rocprofv3 PMC passes of this
-    # same workload and regime (profiles/pmc_traffic.py); null when none matches
-    key = f'{args.config}:{n}:{args.mode}:preroll{preroll}' + (':x_obs' if x_obs else '')
-    for tname in sorted(os.listdir(os.path.join(ROOT, 'profiles')), reverse=True):
-        if not (tname.startswith('r0') and 'pmc_traffic' in tname and tname.endswith('.json')):
-            continue
-        tr_ = json.load(open(os.path.join(ROOT, 'profiles', tname)))
-        if tr_.get('workload') == key:
-            line['roofline']['traffic'] = tr_['traffic_bytes_per_step'] * n_launch / n
-            line['roofline']['traffic_source'] = f'profiles/{tname} (FETCH_SIZE+WRITE_SIZE per mas_step)'
-            break
+    # roofline.traffic: measured in this run only (live_traffic below); null
+    # otherwise (committed PMC files of earlier trees are not this tree's bytes)
     if args.flush_stats:
         env.flush_stats()
         torch.cuda.synchronize()
