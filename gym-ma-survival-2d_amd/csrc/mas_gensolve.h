@@ -289,6 +289,218 @@ __device__ __forceinline__ void island_solve_regs(const Params& P, const SolveRe
     }
 }
 
+// MAS_ISLAND_K=0: every multi-body island through island_solve_regs (A/B).
+// On for the classes with few statics only: the FFA classes' general kernel
+// went 245 -> 256 VGPRs with it and measured 1.2 % slower (r06s), the 2v2
+// class's 2 % faster
+#ifndef MAS_ISLAND_K
+#define MAS_ISLAND_K 1
+#endif
+template <class C>
+constexpr bool kIslandK = MAS_ISLAND_K && C::AM > 2 && C::NS <= 8;
+// island_solve_regs for an island of exactly NB (2 or 3) bodies: the members
+// are gathered into NB compact slots (ascending agent index) and every
+// contact's bodies re-indexed into them once, so each contact step selects
+// out of NB registers instead of AM (one v_cndmask per component instead of
+// AM - 1 to read, NB instead of AM to write back; the agent pair of a
+// two-body island touches slots 0 and 1 with no selection at all).  The same
+// operations on the same values in the same order: the contacts in
+// canonical order, the fixed-point test over the members and the contacts
+// (the other bodies never change), integration and sleep over the members
+// ascending -- so the same bits.
+template <class C, int NB, class KT>
+__device__ __forceinline__ void island_solve_k(const Params& P, const SolveRec<C>& R, const KT& K,
+                                               const int (&qi)[SolveShape<C>::KR], int n, uint32_t members,
+                                               V2 (&c)[C::AM], float (&a)[C::AM], V2 (&v)[C::AM],
+                                               float (&w)[C::AM], float (&sl)[C::AM], float dt, uint32_t& new_awake)
+{
+    constexpr int KC = SolveShape<C>::KR, AM = C::AM;
+    static_assert(NB >= 1 && NB <= AM, "compact islands");  // (NB 1: a dead instantiation of the small classes)
+    const float m = P.inv_mass, Ii = P.inv_I;
+    // the members, ascending, into slots 0..NB-1
+    int idx[NB];
+    {
+        uint32_t mm = members;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            idx[k] = __ffs(mm) - 1;
+            mm &= mm - 1u;
+        }
+    }
+    V2 cc[NB], vv[NB];
+    float aa[NB], ww[NB], ss[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        cc[k] = sel(c, idx[k]);
+        aa[k] = sel(a, idx[k]);
+        vv[k] = sel(v, idx[k]);
+        ww[k] = sel(w, idx[k]);
+        ss[k] = sel(sl, idx[k]);
+    }
+    // slot of agent i among the members (i a member)
+    auto slot_of = [&](int i) { return __popc(members & ((1u << i) - 1u)); };
+    VC k[KC];
+    int key[KC], si[KC], sj[KC];
+    V2 pn[KC], pp[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        const int q = j < n ? qi[j] : 0;
+        k[j].normal = mk(R.at(kRnx, q), R.at(kRny, q));
+        k[j].rA = mk(R.at(kRax, q), R.at(kRay, q));
+        k[j].rB = mk(R.at(kRbx, q), R.at(kRby, q));
+        k[j].nm = R.at(kRnm, q);
+        k[j].tm = R.at(kRtm, q);
+        k[j].ni = R.at(kRni, q);
+        k[j].ti = R.at(kRti, q);
+        key[j] = __float_as_int(R.at(kRkey, q));
+        pn[j] = mk(R.at(kRpnx, q), R.at(kRpny, q));
+        pp[j] = mk(R.at(kRppx, q), R.at(kRppy, q));
+        si[j] = slot_of(slot_i(key[j]));
+        sj[j] = slot_type(key[j]) == 0 ? slot_of(slot_js(key[j])) : 0;
+    }
+    // one contact's velocity step on the compact bodies
+    auto vel = [&](int j, bool warm) {
+        V2 vA = mk(0.0f, 0.0f), vB;
+        float wA = 0.0f, wB;
+        if (slot_type(key[j]) == 0) {
+            if (NB == 2) {  // the pair is slots (0, 1)
+                vA = vv[0]; wA = ww[0];
+                vB = vv[1]; wB = ww[1];
+            } else {
+                vA = sel(vv, si[j]); wA = sel(ww, si[j]);
+                vB = sel(vv, sj[j]); wB = sel(ww, sj[j]);
+            }
+            if (warm) vc_warm(k[j], vA, wA, vB, wB, m, Ii, m, Ii);
+            else vc_solve(k[j], vA, wA, vB, wB, m, Ii, m, Ii);
+            if (NB == 2) {
+                vv[0] = vA; ww[0] = wA;
+                vv[1] = vB; ww[1] = wB;
+            } else {
+                put(vv, si[j], vA); put(ww, si[j], wA);
+                put(vv, sj[j], vB); put(ww, sj[j], wB);
+            }
+        } else {
+            vB = sel(vv, si[j]); wB = sel(ww, si[j]);
+            if (warm) vc_warm(k[j], vA, wA, vB, wB, 0.0f, 0.0f, m, Ii);
+            else vc_solve(k[j], vA, wA, vB, wB, 0.0f, 0.0f, m, Ii);
+            put(vv, si[j], vB); put(ww, si[j], wB);
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < KC; ++j)
+        if (j < n) vel(j, true);
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        V2 vp[NB];
+        float wp[NB], qn[KC], qt[KC];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            vp[b] = vv[b];
+            wp[b] = ww[b];
+        }
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            qn[j] = k[j].ni;
+            qt[j] = k[j].ti;
+        }
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+            if (j < n) vel(j, false);
+        bool same = true;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) same = same && same_bits(vv[b], vp[b]) && same_bits(ww[b], wp[b]);
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+            if (j < n) same = same && same_bits(k[j].ni, qn[j]) && same_bits(k[j].ti, qt[j]);
+        if (same) break;
+    }
+    // store impulses
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        if (j >= n) continue;
+        const int i = slot_i(key[j]), js = slot_js(key[j]);
+        if (slot_type(key[j]) == 0) {
+            const int p = aa_index<AM>(i, js);
+            K.set_aani(p, k[j].ni);
+            K.set_aati(p, k[j].ti);
+        } else {
+            K.set_asni(i, js, k[j].ni);
+            K.set_asti(i, js, k[j].ti);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) integrate(cc[b], aa[b], vv[b], ww[b], dt);
+    bool converged = false;
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        float minsep = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            if (j >= n) continue;
+            float sep;
+            if (slot_type(key[j]) == 0) {
+                V2 cA, cB;
+                float aA, aB;
+                if (NB == 2) {
+                    cA = cc[0]; aA = aa[0];
+                    cB = cc[1]; aB = aa[1];
+                } else {
+                    cA = sel(cc, si[j]); aA = sel(aa, si[j]);
+                    cB = sel(cc, sj[j]); aB = sel(aa, sj[j]);
+                }
+                sep = pc_solve_aa(cA, aA, cB, aB, P.agent_r, m, Ii, kBaumgarte);
+                if (NB == 2) {
+                    cc[0] = cA; aa[0] = aA;
+                    cc[1] = cB; aa[1] = aB;
+                } else {
+                    put(cc, si[j], cA); put(aa, si[j], aA);
+                    put(cc, sj[j], cB); put(aa, sj[j], aB);
+                }
+            } else {
+                V2 cB = sel(cc, si[j]);
+                float aB = sel(aa, si[j]);
+                sep = pc_solve_as_h(pn[j], pp[j], cB, aB, P.agent_r, m, Ii, kBaumgarte, P.inv_mass_rcp);
+                put(cc, si[j], cB); put(aa, si[j], aB);
+            }
+            minsep = fmin_b2(minsep, sep);
+        }
+        if (minsep >= -3.0f * kLinearSlop) {
+            converged = true;
+            break;
+        }
+    }
+    // sleep (island_solve_regs' loop over the members, ascending)
+    const float linTolSqr = kLinSleepTol * kLinSleepTol;
+    const float angTolSqr = kAngSleepTol * kAngSleepTol;
+    float ms = kMaxFloat;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const float ww2 = ww[b] * ww[b], vv2 = dot(vv[b], vv[b]);
+        const bool moving = (ww2 > angTolSqr) | (vv2 > linTolSqr);
+        const float acc = opq(ss[b] + dt);
+        ss[b] = moving ? 0.0f : acc;
+        ms = moving ? 0.0f : fmin_b2(ms, acc);
+    }
+    new_awake = members;
+    if (ms >= kTimeToSleep && converged) {
+        new_awake = 0;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            ss[b] = 0.0f;
+            vv[b] = mk(0.0f, 0.0f);
+            ww[b] = 0.0f;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        put(c, idx[b], cc[b]);
+        put(a, idx[b], aa[b]);
+        put(v, idx[b], vv[b]);
+        put(w, idx[b], ww[b]);
+        put(sl, idx[b], ss[b]);
+    }
+}
+
 // island_solve_regs for an island of ONE body (agent r) and n <= KC contacts,
 // all agent-static: the body stays in scalars instead of being selected out
 // of and put back into the AM-wide arrays around every contact of every
@@ -682,6 +894,8 @@ __device__ __forceinline__ void gen_solve_group(const Params& P, uint32_t* __res
             put(w, r, wr);
             put(sl, r, slr);
             new_awake = asleep ? 0u : members;
+        } else if (nqi <= KC && kIslandK<C> && __popc(members) == 2) {
+            island_solve_k<C, (AM > 2 ? 2 : 1)>(P, R, K, qi, nqi, members, c, a, v, w, sl, dt, new_awake);
         } else if (nqi <= KC) {
             island_solve_regs<C>(P, R, K, qi, nqi, members, c, a, v, w, sl, dt, new_awake);
         } else {

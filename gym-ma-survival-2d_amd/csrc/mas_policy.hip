@@ -409,12 +409,98 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
 constexpr int kHeadN[6] = {3, 3, 3, 2, 2, 2};
 constexpr int kHeadOff[6] = {0, 3, 6, 9, 11, 13};
 
+// The heads' Gumbel-max sampling on both half-waves (the default; the
+// environment's MAS_ACT_SPLIT=0, read per call, selects the one-half loop): lane
+// half 0 holds the rows' 16 outputs (layer 3's padded C tile); lane l + 32
+// takes a copy of lane l's and samples heads 2, 4, 5 while lane l samples
+// heads 0, 1, 3 -- in three slots of equal shape: (0 | 2), (1 | 4, its third
+// logit -inf: it adds nothing to the max, +0 to the exp sum and never wins),
+// (3 | 5) -- so the wave issues the sampling instructions of three heads
+// instead of six.  Each head's max, log-sum-exp, draws (mix64(base + 4 hd +
+// k)) and choice are the same operations on the same values as the one-half
+// loop of k_policy_act, and lane l adds the six heads' terms to the log-prob
+// in head order: the same bits.
+__device__ __forceinline__ void act_sample_split(const f16v& z3, const float* __restrict__ b3, int l, bool ok,
+                                                 int64_t row, uint64_t seed, uint64_t step, int64_t first_row,
+                                                 int8_t* __restrict__ act, float* __restrict__ logp,
+                                                 float* __restrict__ value)
+{
+    const bool hi = l >= 32;
+    float z[kO];
+#pragma unroll
+    for (int o = 0; o < kO; ++o) z[o] = __shfl(z3[o], l & 31, 64) + b3[o];
+    const uint64_t base = mix64(seed ^ mix64(step * 0x100000001B3ULL + (uint64_t)(first_row + row)));
+    constexpr int kA[3] = {0, 1, 3}, kB[3] = {2, 4, 5};
+    float t[3];
+    int bst[3];
+#pragma unroll
+    for (int sl = 0; sl < 3; ++sl) {
+        const int hd = hi ? kB[sl] : kA[sl];
+        const int offA = kHeadOff[kA[sl]], offB = kHeadOff[kB[sl]];
+        constexpr int nn = 3;
+        float zz[nn];
+#pragma unroll
+        for (int k = 0; k < nn; ++k) {
+            const float za = k < kHeadN[kA[sl]] ? z[offA + k] : -INFINITY;
+            const float zb = k < kHeadN[kB[sl]] ? z[offB + k] : -INFINITY;
+            zz[k] = hi ? zb : za;
+        }
+        const int n = hi ? kHeadN[kB[sl]] : kHeadN[kA[sl]];
+        float mx = zz[0];
+#pragma unroll
+        for (int k = 1; k < nn; ++k)
+            if (k < kHeadN[kA[sl]] || k < kHeadN[kB[sl]]) mx = k < n ? fmaxf(mx, zz[k]) : mx;
+        float se = 0.0f;
+#pragma unroll
+        for (int k = 0; k < nn; ++k)
+            if (k < kHeadN[kA[sl]] || k < kHeadN[kB[sl]]) se = k < n ? se + exp_fast(zz[k] - mx) : se;
+        const float lse = mx + log_fast(se);
+        int best = 0;
+        float bv = -INFINITY, lb = zz[0];
+#pragma unroll
+        for (int k = 0; k < nn; ++k) {
+            if (!(k < kHeadN[kA[sl]] || k < kHeadN[kB[sl]])) continue;
+            const uint64_t r = mix64(base + (uint64_t)(hd * 4 + k));
+            const float u = ((float)(r >> 40) + 0.5f) * (1.0f / 16777216.0f);
+            const float g = zz[k] - log_fast(-log_fast(u));
+            if (k < n && g > bv) {
+                bv = g;
+                best = k;
+                lb = zz[k];
+            }
+        }
+        t[sl] = lb - lse;
+        bst[sl] = best;
+    }
+    // lane l gathers heads 2, 4, 5 from lane l + 32 (every lane takes part)
+    const int src = (l & 31) + 32;
+    const float t2 = __shfl(t[0], src, 64), t4 = __shfl(t[1], src, 64), t5 = __shfl(t[2], src, 64);
+    const int bp = __shfl(bst[0] | (bst[1] << 8) | (bst[2] << 16), src, 64);
+    if (hi || !ok) return;
+    float lp = 0.0f;
+    lp += t[0];
+    lp += t[1];
+    lp += t2;
+    lp += t[2];
+    lp += t4;
+    lp += t5;
+    const uint32_t pa0 = (uint32_t)bst[0] | ((uint32_t)bst[1] << 8) | ((uint32_t)(bp & 0xff) << 16) |
+                         ((uint32_t)bst[2] << 24);
+    const uint32_t pa1 = (uint32_t)((bp >> 8) & 0xff) | ((uint32_t)((bp >> 16) & 0xff) << 8);
+    uint16_t* ap = reinterpret_cast<uint16_t*>(act + row * 6);
+    ap[0] = (uint16_t)pa0;
+    ap[1] = (uint16_t)(pa0 >> 16);
+    ap[2] = (uint16_t)pa1;
+    logp[row] = lp;
+    value[row] = z[kO - 1];
+}
+
 // KS > 0: compile-time k-step count (obs_dim in (16 (KS-1), 16 KS]) with every
 // x fragment loaded up front; KS == 0: any obs_dim, chunked layer 1.
 // XIN: the input rows are bf16 rows xb [M][xb_stride] already (mas_step_x
 // wrote them; columns past obs_dim hold the bias column and zeros, which meet
 // W1's zero padding), read instead of fp32 obs and not written back
-template <int KS, bool XIN>
+template <int KS, bool XIN, bool SPLIT = true>
 __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_policy_act(const uint8_t* __restrict__ packed, int D, int ks1,
                                                              int64_t M, const float* __restrict__ obs,
                                                              __bf16* __restrict__ xb, int64_t xb_stride,
@@ -486,6 +572,12 @@ __global__ __launch_bounds__(64 * kWaves, MAS_POL_OCC_ACT * 4 / kWaves) void k_p
     }
     const f16v z3 = layers23<false>(S, F + Lo.w23(), B1 + kMT * 2 * 16, l, on, h1, h2);  // last barrier
     if (!on) return;
+    if constexpr (SPLIT) {
+        if (!(MAS_POL_EXP & 2)) {
+            act_sample_split(z3, B1 + 2 * kMT * 2 * 16, l, ok, row, seed, step, first_row, act, logp, value);
+            return;
+        }
+    }
     if (h != 0 || !ok) return;
     if (MAS_POL_EXP & 2) {
         value[row] = z3[0] + z3[15];
@@ -1858,10 +1950,17 @@ hipError_t policy_act(const void* packed, int D, int64_t M, const float* obs, vo
     const int ks1 = (D + 15) / 16;
     // obs == nullptr: the bf16 rows in xb are the input (mas_policy_act_x)
     const bool xin = obs == nullptr;
-    auto k = xin ? (ks1 == 10 ? pol::k_policy_act<10, true> : ks1 == 9 ? pol::k_policy_act<9, true>
-                                                                       : pol::k_policy_act<0, true>)
-                 : (ks1 == 10 ? pol::k_policy_act<10, false> : ks1 == 9 ? pol::k_policy_act<9, false>
-                                                                        : pol::k_policy_act<0, false>);
+    // the heads' sampling on both half-waves; MAS_ACT_SPLIT=0 (read per call): on one
+    const char* sv = getenv("MAS_ACT_SPLIT");
+    const bool split = !(sv && sv[0] == '0');
+    auto k = split ? (xin ? (ks1 == 10 ? pol::k_policy_act<10, true> : ks1 == 9 ? pol::k_policy_act<9, true>
+                                                                              : pol::k_policy_act<0, true>)
+                          : (ks1 == 10 ? pol::k_policy_act<10, false> : ks1 == 9 ? pol::k_policy_act<9, false>
+                                                                               : pol::k_policy_act<0, false>))
+                   : (xin ? (ks1 == 10 ? pol::k_policy_act<10, true, false> : ks1 == 9 ? pol::k_policy_act<9, true, false>
+                                                                              : pol::k_policy_act<0, true, false>)
+                          : (ks1 == 10 ? pol::k_policy_act<10, false, false>
+                                       : ks1 == 9 ? pol::k_policy_act<9, false, false> : pol::k_policy_act<0, false, false>));
     hipLaunchKernelGGL(k, dim3((unsigned)act_blocks(M)), dim3(64 * pol::kWaves), 0, s, (const uint8_t*)packed, D,
                        ks1, M, obs, (__bf16*)xb, xb_stride, seed, step, first_row, act, logp, value);
     return hipGetLastError();

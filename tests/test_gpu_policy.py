@@ -72,6 +72,35 @@ def test_policy_act_matches_reference(D, M):
     assert agree > 0.97, agree
 
 
+@pytest.mark.parametrize('D,M,first_row', [(160, 262144, 0), (138, 1000 + 13, 77), (160, 32 * 3 + 5, 1 << 20)])
+def test_policy_act_split_sampler_is_bit_identical(D, M, first_row, monkeypatch):
+    """The heads sampled on both half-waves (default) against the one-half
+    loop (MAS_ACT_SPLIT=0): the same actions, log-probs and values, bit for
+    bit, for the fp32-row and the bf16-row (act_x) forms and a shard offset."""
+    p = _policy(D, seed=D + 1)
+    fp = FusedPolicy(p, D, torch.device('cuda'))
+    fp.pack()
+    g = torch.Generator(device='cuda').manual_seed(M)
+    obs = torch.randn((M, D), device='cuda', generator=g) * 3.0
+    xb = fp.x_buffer(M)
+    out = {}
+    for split in ('1', '0'):
+        monkeypatch.setenv('MAS_ACT_SPLIT', split)
+        a = torch.empty((M, 6), dtype=torch.int8, device='cuda')
+        lp = torch.empty((M,), device='cuda')
+        v = torch.empty((M,), device='cuda')
+        fp.act(obs, 5, 123, a, lp, v, xb=xb, first_row=first_row)
+        ax = torch.empty_like(a)
+        lpx = torch.empty_like(lp)
+        vx = torch.empty_like(v)
+        fp.act_x(xb, 5, 124, ax, lpx, vx, first_row=first_row)
+        torch.cuda.synchronize()
+        out[split] = (a, lp, v, ax, lpx, vx)
+    for x, y in zip(out['1'], out['0']):
+        assert torch.equal(x.view(torch.uint8) if x.dtype == torch.int8 else x.view(torch.int32),
+                           y.view(torch.uint8) if y.dtype == torch.int8 else y.view(torch.int32))
+
+
 def test_policy_act_action_distribution():
     D, M = 160, 100000
     p = _policy(D, seed=1, scale=0.0)  # zero weights: the heads' logits are the biases
