@@ -408,6 +408,11 @@ __device__ __forceinline__ bool world_step_fast_lane(AgentL<C>& g, bool alive, b
     return env_ballot<C>(bail) == 0u;
 }
 
+// 1: the agents' body words stored once, after the fast physics (the words
+// before it when the fast path fails); 0: before it too
+#ifndef MAS_PRE_BODY_ONCE
+#define MAS_PRE_BODY_ONCE 1
+#endif
 // waves per SIMD the register budget of k_pre_lanes allows (4: 128 VGPRs, a
 // 12-register spill for 2v2; 3: 168, none)
 #ifndef MAS_PRE_OCC
@@ -708,11 +713,18 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
     const uint32_t awake_pre = env_ballot<C>(awake) | (awake_m0 & ~((AM >= 32) ? 0xffffffffu : ((1u << AM) - 1u)));
     // (every ballot in uniform control flow: a ballot counts active lanes only)
     const uint32_t heals_used = env_ballot<C>(use_heal), boxes_used = env_ballot<C>(use_box);
+#if MAS_PRE_BODY_ONCE
+    // the body words before the fast physics: stored below, once, only when
+    // the fast path fails (the general path restarts from them)
+    const float dpre[7] = {g.c.x, g.c.y, g.a, g.v.x, g.v.y, g.w, g.sleep};
+#endif
     if (valid) {
+#if !MAS_PRE_BODY_ONCE
         const float d[7] = {g.c.x, g.c.y, g.a, g.v.x, g.v.y, g.w, g.sleep};
 #pragma unroll
         for (int q = 0; q < 7; ++q) state[state_index(7 * i + q, e, N)] = __float_as_uint(d[q]);
         if (i == 0) state[state_index(LY::awake, e, N)] = awake_pre;
+#endif
         if (dirty_env & kGRule) {
             const int wr = LY::rule + i * LY::kRuleA;
             state[state_index(wr, e, N)] = (uint32_t)g.health;
@@ -772,6 +784,13 @@ __global__ __launch_bounds__(kWG, MAS_PRE_OCC) void k_pre_lanes(Params P, uint32
             }
         }
     }
+#if MAS_PRE_BODY_ONCE
+    if (!ok && valid) {
+#pragma unroll
+        for (int q = 0; q < 7; ++q) state[state_index(7 * i + q, e, N)] = __float_as_uint(dpre[q]);
+        if (i == 0) state[state_index(LY::awake, e, N)] = awake_pre;
+    }
+#endif
     MAS_PROF(P, 24);
     // the general-path list append and the slow routing, one lane per env
     const bool lead = i == 0 && valid;
